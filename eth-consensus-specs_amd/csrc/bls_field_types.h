@@ -1,0 +1,30 @@
+// Field / point storage types for the MI355X BLS12-381 backend.
+//
+// Fp is one 381-bit residue in Montgomery form (R = 2^384) held as 12 x 32-bit
+// little-endian limbs: exactly the operand width of v_mad_u64_u32, so one limb
+// product is one instruction.  Every arithmetic routine is __host__ __device__
+// so the same source is unit-tested on the host (tests/hostcheck) and run in
+// the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BLS_HD __host__ __device__ __forceinline__
+#define BLS_HDNI __host__ __device__ __noinline__
+
+namespace bls {
+
+struct Fp {
+  uint32_t l[12];
+};
+struct Fp2 {
+  Fp c0, c1;  // c0 + c1 * i,  i^2 = -1
+};
+struct Fp6 {
+  Fp2 c0, c1, c2;  // c0 + c1 v + c2 v^2,  v^3 = xi = 1 + i
+};
+struct Fp12 {
+  Fp6 c0, c1;  // c0 + c1 w,  w^2 = v
+};
+
+}  // namespace bls

@@ -1,0 +1,76 @@
+"""ctypes wrapper for tests/hostcheck/libhostcheck.so (TEST HARNESS ONLY).
+
+The library is a host (CPU) build of the same device headers the HIP kernels
+use; it lets the arithmetic be checked against ``oracle/`` without a GPU.  The
+product shim never loads it.
+"""
+import ctypes
+import os
+import subprocess
+
+from oracle import bls_oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "hostcheck", "hostcheck.cpp")
+LIB = os.path.join(HERE, "hostcheck", "libhostcheck.so")
+INC = os.path.join(ROOT, "eth-consensus-specs_amd", "csrc")
+
+
+def build(force=False):
+    deps = [SRC] + [os.path.join(INC, f) for f in os.listdir(INC) if f.endswith(".h")]
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
+        return LIB
+    subprocess.check_call(["hipcc", "-x", "hip", "--offload-host-only", "-O2", "-fPIC", "-shared", "-I", INC,
+                           "-o", LIB, SRC], timeout=900)
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+    return _lib
+
+
+def fp_b(v):
+    return (v % O.P).to_bytes(48, "big")
+
+
+def fp2_b(a):
+    return fp_b(a[0]) + fp_b(a[1])
+
+
+def b_fp(b):
+    return int.from_bytes(b[:48], "big")
+
+
+def b_fp2(b):
+    return (b_fp(b[:48]), b_fp(b[48:96]))
+
+
+def fp12_b(a):
+    return b"".join(fp2_b(c) for c in O.f12_to_coeffs(a))
+
+
+def b_fp12(b):
+    return O.f12_from_coeffs([b_fp2(b[96 * k: 96 * k + 96]) for k in range(6)])
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def call(name, *args, out=0, ret=False):
+    f = getattr(lib(), name)
+    o = buf(out) if out else None
+    a = list(args) + ([o] if out else [])
+    r = f(*a)
+    if out and ret:
+        return r, o.raw
+    if out:
+        return o.raw
+    return r

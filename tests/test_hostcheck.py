@@ -1,0 +1,188 @@
+"""Host build of the device arithmetic (tests/hostcheck) vs the CPU oracle.
+
+Runs on CPU: it compiles the same headers the gfx950 kernels use for the host
+and compares every layer (Fp .. pairing, hash_to_G2, decode) with oracle/.
+"""
+import random
+
+import pytest
+
+from oracle import bls_oracle as O
+import _hostcheck as H
+
+rng = random.Random(0x5EED)
+
+
+def rfp():
+    return rng.randrange(O.P)
+
+
+def rfp2():
+    return (rfp(), rfp())
+
+
+def rfp12():
+    return O.f12_from_coeffs([rfp2() for _ in range(6)])
+
+
+def test_fp_ops():
+    for _ in range(200):
+        a, b = rfp(), rfp()
+        assert H.b_fp(H.call("hc_fp_mul", H.fp_b(a), H.fp_b(b), out=48)) == a * b % O.P
+        assert H.b_fp(H.call("hc_fp_add", H.fp_b(a), H.fp_b(b), out=48)) == (a + b) % O.P
+        assert H.b_fp(H.call("hc_fp_sub", H.fp_b(a), H.fp_b(b), out=48)) == (a - b) % O.P
+    for a in (1, 2, O.P - 1, rfp()):
+        assert H.b_fp(H.call("hc_fp_inv", H.fp_b(a), out=48)) == pow(a, -1, O.P)
+    # edge operands
+    for a, b in ((0, 0), (O.P - 1, O.P - 1), (0, O.P - 1), (1, O.P - 1)):
+        assert H.b_fp(H.call("hc_fp_mul", H.fp_b(a), H.fp_b(b), out=48)) == a * b % O.P
+        assert H.b_fp(H.call("hc_fp_add", H.fp_b(a), H.fp_b(b), out=48)) == (a + b) % O.P
+        assert H.b_fp(H.call("hc_fp_sub", H.fp_b(a), H.fp_b(b), out=48)) == (a - b) % O.P
+
+
+def test_fp2_ops():
+    for _ in range(50):
+        a, b = rfp2(), rfp2()
+        assert H.b_fp2(H.call("hc_fp2_mul", H.fp2_b(a), H.fp2_b(b), out=96)) == O.f2_mul(a, b)
+        assert H.b_fp2(H.call("hc_fp2_sqr", H.fp2_b(a), out=96)) == O.f2_sqr(a)
+        assert H.b_fp2(H.call("hc_fp2_inv", H.fp2_b(a), out=96)) == O.f2_inv(a)
+        sq = O.f2_sqr(a)
+        ok, r = H.call("hc_fp2_sqrt", H.fp2_b(sq), out=96, ret=True)
+        assert ok == 1 and O.f2_sqr(H.b_fp2(r)) == sq
+    # real / imaginary-only squares and a non-square
+    for a in ((5, 0), (0, 7), (rfp(), 0)):
+        sq = O.f2_sqr(a)
+        ok, r = H.call("hc_fp2_sqrt", H.fp2_b(sq), out=96, ret=True)
+        assert ok == 1 and O.f2_sqr(H.b_fp2(r)) == sq
+    ns = next(x for x in (rfp2() for _ in range(100)) if not O.f2_is_square(x))
+    ok, _ = H.call("hc_fp2_sqrt", H.fp2_b(ns), out=96, ret=True)
+    assert ok == 0
+
+
+def test_fp12_ops():
+    for _ in range(4):
+        a, b = rfp12(), rfp12()
+        assert H.b_fp12(H.call("hc_fp12_mul", H.fp12_b(a), H.fp12_b(b), out=576)) == O.f12_mul(a, b)
+        assert H.b_fp12(H.call("hc_fp12_sqr", H.fp12_b(a), out=576)) == O.f12_sqr(a)
+        assert H.b_fp12(H.call("hc_fp12_inv", H.fp12_b(a), out=576)) == O.f12_inv(a)
+        assert H.b_fp12(H.call("hc_fp12_frob1", H.fp12_b(a), out=576)) == O.f12_frobenius(a)
+        assert H.b_fp12(H.call("hc_fp12_frob2", H.fp12_b(a), out=576)) == O.f12_frobenius(O.f12_frobenius(a))
+        l0, l2, l3 = rfp2(), rfp2(), rfp2()
+        line = O.f12_from_coeffs([l0, O.F2_ZERO, l2, l3, O.F2_ZERO, O.F2_ZERO])
+        got = H.b_fp12(H.call("hc_fp12_mul_line", H.fp12_b(a), H.fp2_b(l0), H.fp2_b(l2), H.fp2_b(l3), out=576))
+        assert got == O.f12_mul(a, line)
+
+
+def test_frobenius_is_pow_p():
+    a = rfp12()
+    assert O.f12_frobenius(a) == O.f12_pow(a, O.P)
+
+
+def _g1b(pt):
+    return H.fp_b(pt[0]) + H.fp_b(pt[1])
+
+
+def _g2b(pt):
+    return H.fp2_b(pt[0]) + H.fp2_b(pt[1])
+
+
+def test_miller_loop_and_final_exp():
+    p = O.g1_mul(O.G1_GEN, 0x1234567)
+    q = O.g2_mul(O.G2_GEN, 0x7654321)
+    f = H.b_fp12(H.call("hc_miller_loop", _g1b(p), _g2b(q), out=576))
+    # the device Miller loop differs from the textbook one by subfield factors only
+    assert O.final_exponentiation(f) == O.pairing(p, q)
+    g = H.b_fp12(H.call("hc_final_exp", H.fp12_b(f), out=576))
+    e = O.final_exponentiation(f)
+    assert g == O.f12_mul(O.f12_mul(e, e), e)  # device hard part computes e^3
+
+
+def test_decode_and_subgroup():
+    for k in (1, 2, 0xDEADBEEF):
+        pt = O.g1_mul(O.G1_GEN, k)
+        enc = O.g1_compress(pt)
+        st, out = H.call("hc_g1_decompress", enc, out=96, ret=True)
+        assert st == 0 and (H.b_fp(out[:48]), H.b_fp(out[48:])) == pt
+        assert H.call("hc_g1_in_subgroup", _g1b(pt)) == 1
+        q = O.g2_mul(O.G2_GEN, k)
+        st, out = H.call("hc_g2_decompress", O.g2_compress(q), out=192, ret=True)
+        assert st == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == q
+        assert H.call("hc_g2_in_subgroup", _g2b(q)) == 1
+    # points on the curves but outside the prime-order subgroups
+    x = 1
+    while True:
+        y = O.fp_sqrt(x ** 3 + 4)
+        if y is not None and not O.g1_in_subgroup((x, y)):
+            break
+        x += 1
+    assert H.call("hc_g1_in_subgroup", _g1b((x, y))) == 0
+    q = O.iso_map(O.map_to_curve_sswu((3, 4)))
+    assert not O.g2_in_subgroup(q)
+    assert H.call("hc_g2_in_subgroup", _g2b(q)) == 0
+
+
+@pytest.mark.parametrize("enc,status", [
+    (bytes(48), 2),                                   # c_flag clear
+    (bytes([0xC0]) + bytes(47), 1),                   # infinity
+    (bytes([0x80]) + bytes(47), 2),                   # x == 0 without b_flag
+    (bytes([0xE0]) + bytes(47), 2),                   # infinity with a_flag
+    (bytes([0xC0, 0x10]) + bytes(46), 2),             # b_flag with x != 0
+    (bytes([0x40]) + bytes(47), 2),                   # b_flag without c_flag
+    ((O.P | (1 << 383)).to_bytes(48, "big"), 3),      # x == p
+    (bytes([0x9F]) + b"\xff" * 47, 3),                # x > p
+])
+def test_g1_decode_edges(enc, status):
+    st, _ = H.call("hc_g1_decompress", enc, out=96, ret=True)
+    assert st == status
+    with pytest.raises(O.DecodeError) if status >= 2 else _nullctx():
+        O.g1_decompress(enc)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def test_g1_not_on_curve():
+    x = 1
+    while O.fp_sqrt(x ** 3 + 4) is not None:
+        x += 1
+    enc = (x | (1 << 383)).to_bytes(48, "big")
+    st, _ = H.call("hc_g1_decompress", enc, out=96, ret=True)
+    assert st == 4
+
+
+def test_expand_and_hash_to_field():
+    for msg in (b"", b"abc", bytes(32), b"\x12" * 32, bytes(range(200))):
+        dst = O.DST_POP
+        ub = H.call("hc_expand_message_xmd", msg, len(msg), dst, len(dst), out=256)
+        assert ub == O.expand_message_xmd(msg, dst, 256)
+        u = H.call("hc_hash_to_field", msg, len(msg), dst, len(dst), out=192)
+        assert [H.b_fp2(u[:96]), H.b_fp2(u[96:])] == O.hash_to_field_fp2(msg, 2, dst)
+
+
+def test_expand_message_rfc9380_vector():
+    # RFC 9380 App. K.1 (expand_message_xmd SHA-256, DST QUUX-V01-CS02-with-expander-SHA256-128), msg="" len 0x20
+    dst = b"QUUX-V01-CS02-with-expander-SHA256-128"
+    assert O.expand_message_xmd(b"", dst, 0x20).hex() == "68a985b87eb6b46952128911f2a4412bbc302a9d759667f87f7a21d803f07235"
+
+
+def test_map_to_curve_and_hash_to_g2():
+    for _ in range(3):
+        u = rfp2()
+        out = H.call("hc_map_to_curve", H.fp2_b(u), out=192)
+        assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
+    for msg in (b"", bytes(32), b"\x56" * 32, b"hello world"):
+        got = H.call("hc_hash_to_g2", msg, len(msg), O.DST_POP, len(O.DST_POP), out=96)
+        assert got == O.g2_compress(O.hash_to_g2(msg))
+
+
+def test_core_verify_known_answer():
+    from golden_data import DEPOSIT_CLI
+    pk, root, sig = DEPOSIT_CLI["pubkey"], DEPOSIT_CLI["signing_root"], DEPOSIT_CLI["signature"]
+    assert H.call("hc_core_verify", pk, root, 32, O.DST_POP, len(O.DST_POP), sig) == 1
+    bad = bytes([root[0] ^ 1]) + root[1:]
+    assert H.call("hc_core_verify", pk, bad, 32, O.DST_POP, len(O.DST_POP), sig) == 0
