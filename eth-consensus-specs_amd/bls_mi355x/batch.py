@@ -1,0 +1,171 @@
+"""Batch / registry API (the throughput path).
+
+The per-call drop-in API (``backend.mi355x_bls``) verifies one signature per
+ctypes call.  Spec call sites that verify many aggregates against the
+validator registry (``is_valid_indexed_attestation``,
+specs/phase0/beacon-chain.md:776-790; ``process_sync_aggregate``,
+specs/altair/beacon-chain.md:575-610) use these instead: the registry's
+pubkeys are decoded and KeyValidated once into HBM and each aggregate is
+named by registry indices.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _native
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(b) -> np.ndarray:
+    return np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else np.ascontiguousarray(b, np.uint8)
+
+
+class Registry:
+    """HBM-resident affine pubkey table of one context."""
+
+    def __init__(self, ctx: _native.Context | None = None):
+        self.ctx = ctx or _native.context()
+
+    def load(self, pubkeys48: bytes | np.ndarray) -> np.ndarray:
+        """Decode + KeyValidate ``n`` compressed keys; returns the validity mask."""
+        buf = _u8(pubkeys48)
+        if buf.size % 48:
+            raise ValueError("pubkeys must be a multiple of 48 bytes")
+        n = buf.size // 48
+        valid = np.zeros(n, dtype=np.uint8)
+        c = self.ctx
+        c.check(c.lib.bls_registry_load(c.h, buf.tobytes(), n, _ptr(valid)))
+        return valid
+
+    def __len__(self):
+        return int(self.ctx.lib.bls_registry_size(self.ctx.h))
+
+
+def offsets_from_lengths(lengths) -> np.ndarray:
+    offs = np.zeros(len(lengths) + 1, dtype=np.uint64)
+    np.cumsum(np.asarray(lengths, dtype=np.uint64), out=offs[1:])
+    return offs
+
+
+def fast_aggregate_verify_batch(indices: np.ndarray, offsets: np.ndarray, msgs32, sigs96, ctx=None) -> np.ndarray:
+    """B FastAggregateVerify calls over registry indices -> bool array."""
+    c = ctx or _native.context()
+    idx = np.ascontiguousarray(indices, dtype=np.uint32)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    B = offs.size - 1
+    m, s = _u8(msgs32), _u8(sigs96)
+    if m.size != 32 * B or s.size != 96 * B:
+        raise ValueError("need 32-byte messages and 96-byte signatures, one per aggregate")
+    out = np.zeros(B, dtype=np.uint8)
+    c.check(c.lib.bls_fav_batch_indexed(c.h, _ptr(idx), _ptr(offs), B, m.tobytes(), s.tobytes(), _ptr(out)))
+    return out.astype(bool)
+
+
+def verify_batch(indices: np.ndarray, msgs32, sigs96, ctx=None) -> np.ndarray:
+    """B Verify calls with registry-resident pubkeys -> bool array."""
+    c = ctx or _native.context()
+    idx = np.ascontiguousarray(indices, dtype=np.uint32)
+    B = idx.size
+    m, s = _u8(msgs32), _u8(sigs96)
+    if m.size != 32 * B or s.size != 96 * B:
+        raise ValueError("need 32-byte messages and 96-byte signatures")
+    out = np.zeros(B, dtype=np.uint8)
+    c.check(c.lib.bls_verify_batch_indexed(c.h, _ptr(idx), B, m.tobytes(), s.tobytes(), _ptr(out)))
+    return out.astype(bool)
+
+
+def sign_batch(sks32, msgs32, ctx=None) -> bytes:
+    c = ctx or _native.context()
+    sk, m = _u8(sks32), _u8(msgs32)
+    B = sk.size // 32
+    out = ctypes.create_string_buffer(96 * B)
+    if c.check(c.lib.bls_sign_batch(c.h, sk.tobytes(), m.tobytes(), B, out)) != 1:
+        raise ValueError("invalid secret key in batch")
+    return out.raw
+
+
+def sk_to_pk_batch(sks32, ctx=None) -> bytes:
+    c = ctx or _native.context()
+    sk = _u8(sks32)
+    B = sk.size // 32
+    out = ctypes.create_string_buffer(48 * B)
+    if c.check(c.lib.bls_sk_to_pk_batch(c.h, sk.tobytes(), B, out)) != 1:
+        raise ValueError("invalid secret key in batch")
+    return out.raw
+
+
+class DeviceBuffer:
+    """HBM buffer owned by a context (inputs resident before a timed region)."""
+
+    def __init__(self, ctx: _native.Context, data: np.ndarray | bytes | None = None, nbytes: int | None = None):
+        self.ctx = ctx
+        arr = None if data is None else (np.ascontiguousarray(data) if isinstance(data, np.ndarray) else _u8(data))
+        self.nbytes = int(arr.nbytes if arr is not None else nbytes)
+        self.ptr = ctx.lib.bls_dev_alloc(ctx.h, max(self.nbytes, 1))
+        if not self.ptr:
+            raise _native.NativeError("bls_dev_alloc failed")
+        if arr is not None and self.nbytes:
+            ctx.check(ctx.lib.bls_h2d(ctx.h, self.ptr, _ptr(arr), self.nbytes))
+
+    def to_host(self) -> np.ndarray:
+        out = np.empty(self.nbytes, dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.bls_d2h(self.ctx.h, _ptr(out), self.ptr, self.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            self.ctx.lib.bls_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+
+class ResidentFavBatch:
+    """A FastAggregateVerify batch whose inputs live in HBM (bench / multi-GPU).
+
+    ``partial()`` runs this shard's checks and Miller loops and returns the
+    576-byte Fp12 partial; partials of all shards are multiplied and
+    final-exponentiated by ``check_partials``; ``finish()`` writes verdicts.
+    """
+
+    def __init__(self, indices, offsets, msgs32, sigs96, ctx=None):
+        self.ctx = ctx or _native.context()
+        self.idx = DeviceBuffer(self.ctx, np.ascontiguousarray(indices, dtype=np.uint32))
+        self.offs = DeviceBuffer(self.ctx, np.ascontiguousarray(offsets, dtype=np.uint64))
+        self.B = int(np.asarray(offsets).size - 1)
+        self.msgs = DeviceBuffer(self.ctx, _u8(msgs32))
+        self.sigs = DeviceBuffer(self.ctx, _u8(sigs96))
+        self.out = DeviceBuffer(self.ctx, nbytes=self.B)
+
+    def partial(self, seed32: bytes | None = None) -> bytes:
+        seed = seed32 if seed32 is not None else os.urandom(32)
+        buf = ctypes.create_string_buffer(576)
+        c = self.ctx
+        c.check(c.lib.bls_fav_batch_partial_dev(c.h, self.idx.ptr, self.offs.ptr, self.B, self.msgs.ptr,
+                                                self.sigs.ptr, seed, buf))
+        return buf.raw
+
+    def check_partials(self, partials: bytes) -> bool:
+        c = self.ctx
+        n = len(partials) // 576
+        return c.check(c.lib.bls_partials_check(c.h, partials, n)) == 1
+
+    def finish(self, batch_ok: bool) -> None:
+        c = self.ctx
+        c.check(c.lib.bls_fav_batch_finish_dev(c.h, 1 if batch_ok else 0, self.out.ptr))
+
+    def verdicts(self) -> np.ndarray:
+        return self.out.to_host().astype(bool)
+
+    def run(self) -> np.ndarray:
+        ok = self.check_partials(self.partial())
+        self.finish(ok)
+        return self.verdicts()
+
+    def free(self):
+        for b in (self.idx, self.offs, self.msgs, self.sigs, self.out):
+            b.free()

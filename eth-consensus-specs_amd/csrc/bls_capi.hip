@@ -1,0 +1,653 @@
+// C ABI of libblsmi355x.so (declared in include/blsmi355x.h).  Host code:
+// argument checks, H2D/D2H copies into a per-context scratch arena, kernel
+// launches on the context's stream.  No compute happens on the host.
+#include <mutex>
+#include <new>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "../../include/blsmi355x.h"
+#include "bls_kernels.h"
+
+using namespace bls;
+
+namespace {
+
+enum Slot {
+  S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
+  // FAV batch state (kept between partial and finish)
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK,
+  NSLOT
+};
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct bls_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  Buf buf[NSLOT];
+  // registry (HBM resident)
+  G1A* reg = nullptr;
+  uint8_t* reg_ok = nullptr;
+  size_t reg_n = 0;
+  // last prepared FAV batch
+  size_t fav_B = 0;
+  bool fav_ready = false;
+};
+
+namespace {
+
+int fail(bls_ctx* c, hipError_t e, const char* where) {
+  char b[256];
+  snprintf(b, sizeof b, "%s: %s", where, hipGetErrorString(e));
+  c->err = b;
+  return BLS_E_DEVICE;
+}
+
+#define HIPCK(x)                                     \
+  do {                                               \
+    hipError_t e_ = (x);                             \
+    if (e_ != hipSuccess) return fail(ctx, e_, #x); \
+  } while (0)
+
+// Device scratch pointer for slot s with at least `bytes` bytes.
+template <class T>
+int scratch(bls_ctx* ctx, int s, size_t count, T** out) {
+  size_t bytes = count * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  Buf& b = ctx->buf[s];
+  if (b.cap < bytes) {
+    if (b.p) {
+      HIPCK(hipStreamSynchronize(ctx->stream));
+      HIPCK(hipFree(b.p));
+      b.p = nullptr;
+      b.cap = 0;
+    }
+    size_t cap = bytes + bytes / 4;
+    HIPCK(hipMalloc(&b.p, cap));
+    b.cap = cap;
+  }
+  *out = (T*)b.p;
+  return 0;
+}
+
+#define SCR(slot, n, ptr)                       \
+  do {                                          \
+    int r_ = scratch(ctx, slot, (n), &(ptr));   \
+    if (r_) return r_;                          \
+  } while (0)
+
+int h2d(bls_ctx* ctx, void* d, const void* h, size_t n) {
+  if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, ctx->stream));
+  return 0;
+}
+int d2h(bls_ctx* ctx, void* h, const void* d, size_t n) {
+  if (n) HIPCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+#define CK(x)            \
+  do {                   \
+    int r_ = (x);        \
+    if (r_) return r_;   \
+  } while (0)
+#define LK(x)                                                   \
+  do {                                                          \
+    hipError_t e_ = (x);                                        \
+    if (e_ != hipSuccess) return fail(ctx, e_, #x);             \
+  } while (0)
+
+// Copy n compressed keys, validate them on the device; returns 1 if all valid.
+int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** outOk) {
+  uint8_t* d_in;
+  G1A* d_a;
+  int* d_ok;
+  SCR(S_IN0, 48 * n, d_in);
+  SCR(S_G1A, n + 1, d_a);
+  SCR(S_OK, n + 1, d_ok);
+  CK(h2d(ctx, d_in, pks, 48 * n));
+  LK(launch_key_validate(ctx->stream, d_in, n, d_a, d_ok));
+  std::vector<int> ok(n);
+  CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
+  *outA = d_a;
+  *outOk = d_ok;
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) return 0;
+  return 1;
+}
+
+int run_final_check(bls_ctx* ctx, const Fp12* f) {
+  int* d_r;
+  SCR(S_INT, 4, d_r);
+  LK(launch_final_check(ctx->stream, f, d_r));
+  int r = 0;
+  CK(d2h(ctx, &r, d_r, sizeof r));
+  return r ? 1 : 0;
+}
+
+__global__ void k_set_neg_g1(G1A* p) {
+  if (threadIdx.x || blockIdx.x) return;
+  G1A g = g1_generator();
+  g.y = fp_neg(g.y);
+  *p = g;
+}
+
+}  // namespace
+
+#define API_ENTER(ctx)                         \
+  if (!ctx) return BLS_E_ARG;                  \
+  std::lock_guard<std::mutex> lock_(ctx->mu);  \
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, hipGetLastError(), "hipSetDevice")
+
+extern "C" {
+
+int bls_ctx_create(int device, bls_ctx** out) {
+  if (!out) return BLS_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return BLS_E_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return BLS_E_DEVICE;
+  bls_ctx* c = new (std::nothrow) bls_ctx();
+  if (!c) return BLS_E_DEVICE;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return BLS_E_DEVICE;
+  }
+  *out = c;
+  return 0;
+}
+
+void bls_ctx_destroy(bls_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& b : ctx->buf)
+    if (b.p) (void)hipFree(b.p);
+  if (ctx->reg) (void)hipFree(ctx->reg);
+  if (ctx->reg_ok) (void)hipFree(ctx->reg_ok);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* bls_last_error(bls_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
+  API_ENTER(ctx);
+  hipDeviceProp_t p;
+  HIPCK(hipGetDeviceProperties(&p, ctx->device));
+  if (name && name_len) {
+    snprintf(name, name_len, "%s (%s)", p.name, p.gcnArchName);
+  }
+  if (cu_count) *cu_count = p.multiProcessorCount;
+  return 0;
+}
+
+int bls_verify(bls_ctx* ctx, const uint8_t* pk48, const uint8_t* msg, size_t msg_len, const uint8_t* sig96) {
+  API_ENTER(ctx);
+  if (!pk48 || !sig96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
+  uint8_t* d;
+  int* d_r;
+  SCR(S_IN0, 48 + 96 + msg_len, d);
+  SCR(S_INT, 4, d_r);
+  CK(h2d(ctx, d, pk48, 48));
+  CK(h2d(ctx, d + 48, sig96, 96));
+  CK(h2d(ctx, d + 144, msg, msg_len));
+  LK(launch_verify_single(ctx->stream, d, d + 144, (uint32_t)msg_len, d + 48, d_r));
+  int r = 0;
+  CK(d2h(ctx, &r, d_r, sizeof r));
+  return r ? 1 : 0;
+}
+
+int bls_fast_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
+                              const uint8_t* sig96) {
+  API_ENTER(ctx);
+  if ((!pks48 && n) || !sig96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
+  if (n == 0) return 0;
+  G1A* a;
+  int* ok;
+  int v = validate_pks(ctx, pks48, n, &a, &ok);
+  if (v <= 0) return v;
+  G1J *tmp, *apk;
+  uint8_t* d;
+  int* d_r;
+  SCR(S_G1J_T, 1024, tmp);
+  SCR(S_G1J, 1, apk);
+  SCR(S_IN1, 96 + msg_len, d);
+  SCR(S_INT, 4, d_r);
+  LK(launch_g1_sum_aff(ctx->stream, a, nullptr, n, tmp, apk));
+  CK(h2d(ctx, d, sig96, 96));
+  CK(h2d(ctx, d + 96, msg, msg_len));
+  LK(launch_verify_apk(ctx->stream, apk, d + 96, (uint32_t)msg_len, d, d_r));
+  int r = 0;
+  CK(d2h(ctx, &r, d_r, sizeof r));
+  return r ? 1 : 0;
+}
+
+int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msgs, const size_t* msg_lens,
+                         const uint8_t* sig96) {
+  API_ENTER(ctx);
+  if ((!pks48 || !msg_lens) && n) return BLS_E_ARG;
+  if (!sig96) return BLS_E_ARG;
+  if (n == 0) return 0;
+  std::vector<uint64_t> offs(n + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    if (msg_lens[i] > 0xffffffffu) return BLS_E_ARG;
+    offs[i + 1] = offs[i] + msg_lens[i];
+  }
+  if (offs[n] && !msgs) return BLS_E_ARG;
+  G1A* P;
+  int* ok;
+  int v = validate_pks(ctx, pks48, n, &P, &ok);
+  if (v <= 0) return v;
+  uint8_t *d_sig, *d_msgs;
+  uint64_t* d_offs;
+  G2A* Q;
+  int* d_sok;
+  Fp12 *f, *ft, *fo;
+  SCR(S_IN1, 96, d_sig);
+  SCR(S_IN2, offs[n], d_msgs);
+  SCR(S_OFFS, n + 1, d_offs);
+  SCR(S_G2A, n + 1, Q);
+  SCR(S_INT, 4, d_sok);
+  SCR(S_F, n + 1, f);
+  SCR(S_F_T, 512, ft);
+  SCR(S_FPART, 1, fo);
+  CK(h2d(ctx, d_sig, sig96, 96));
+  LK(launch_sig_validate(ctx->stream, d_sig, 1, Q + n, d_sok));
+  int sok = 0;
+  CK(d2h(ctx, &sok, d_sok, sizeof sok));
+  if (!sok) return 0;
+  CK(h2d(ctx, d_msgs, msgs, offs[n]));
+  CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
+  LK(launch_hash_many(ctx->stream, d_msgs, d_offs, n, nullptr, 0, Q));
+  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->stream, P + n);
+  LK(hipGetLastError());
+  LK(launch_miller(ctx->stream, P, Q, nullptr, n + 1, f));
+  LK(launch_fp12_prod(ctx->stream, f, n + 1, ft, fo));
+  return run_final_check(ctx, fo);
+}
+
+int bls_aggregate(bls_ctx* ctx, const uint8_t* sigs96, size_t n, uint8_t* out96) {
+  API_ENTER(ctx);
+  if ((!sigs96 && n) || !out96) return BLS_E_ARG;
+  if (n == 0) return 0;
+  uint8_t *d_in, *d_out;
+  G2A* a;
+  int* d_ok;
+  G2J *tmp, *s;
+  SCR(S_IN0, 96 * n, d_in);
+  SCR(S_G2A, n, a);
+  SCR(S_OK, n, d_ok);
+  SCR(S_G2J_T, 1024, tmp);
+  SCR(S_G2J, 1, s);
+  SCR(S_IN1, 96, d_out);
+  CK(h2d(ctx, d_in, sigs96, 96 * n));
+  LK(launch_sig_validate(ctx->stream, d_in, n, a, d_ok));
+  std::vector<int> ok(n);
+  CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) return 0;
+  LK(launch_g2_sum_aff(ctx->stream, a, nullptr, n, tmp, s));
+  LK(launch_g2_compress(ctx->stream, s, d_out));
+  CK(d2h(ctx, out96, d_out, 96));
+  return 1;
+}
+
+int bls_aggregate_pks(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out48) {
+  API_ENTER(ctx);
+  if ((!pks48 && n) || !out48) return BLS_E_ARG;
+  if (n == 0) return 0;
+  G1A* a;
+  int* ok;
+  int v = validate_pks(ctx, pks48, n, &a, &ok);
+  if (v <= 0) return v;
+  G1J *tmp, *s;
+  uint8_t* d_out;
+  SCR(S_G1J_T, 1024, tmp);
+  SCR(S_G1J, 1, s);
+  SCR(S_IN1, 48, d_out);
+  LK(launch_g1_sum_aff(ctx->stream, a, nullptr, n, tmp, s));
+  LK(launch_g1_compress(ctx->stream, s, d_out, nullptr));
+  CK(d2h(ctx, out48, d_out, 48));
+  return 1;
+}
+
+int bls_key_validate(bls_ctx* ctx, const uint8_t* pk48) {
+  API_ENTER(ctx);
+  if (!pk48) return BLS_E_ARG;
+  G1A* a;
+  int* ok;
+  return validate_pks(ctx, pk48, 1, &a, &ok);
+}
+
+static int sign_impl(bls_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n,
+                     uint8_t* out96, int* all_ok) {
+  uint8_t *d_sk, *d_m, *d_out;
+  uint64_t* d_offs;
+  int* d_ok;
+  SCR(S_IN0, 32 * n, d_sk);
+  SCR(S_IN1, offs[n], d_m);
+  SCR(S_IN2, 96 * n, d_out);
+  SCR(S_OFFS, n + 1, d_offs);
+  SCR(S_OK, n, d_ok);
+  CK(h2d(ctx, d_sk, sks, 32 * n));
+  CK(h2d(ctx, d_m, msgs, offs[n]));
+  CK(h2d(ctx, d_offs, offs, (n + 1) * sizeof(uint64_t)));
+  LK(launch_sign_many(ctx->stream, d_sk, d_m, d_offs, n, d_out, d_ok));
+  std::vector<int> ok(n);
+  CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
+  CK(d2h(ctx, out96, d_out, 96 * n));
+  *all_ok = 1;
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) *all_ok = 0;
+  return 0;
+}
+
+int bls_sign(bls_ctx* ctx, const uint8_t* sk32, const uint8_t* msg, size_t msg_len, uint8_t* out96) {
+  API_ENTER(ctx);
+  if (!sk32 || !out96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
+  uint64_t offs[2] = {0, msg_len};
+  int ok = 0;
+  CK(sign_impl(ctx, sk32, msg, offs, 1, out96, &ok));
+  return ok;
+}
+
+int bls_sign_batch(bls_ctx* ctx, const uint8_t* sks32, const uint8_t* msgs32, size_t B, uint8_t* out96) {
+  API_ENTER(ctx);
+  if ((!sks32 || !msgs32 || !out96) && B) return BLS_E_ARG;
+  if (!B) return 1;
+  std::vector<uint64_t> offs(B + 1);
+  for (size_t i = 0; i <= B; i++) offs[i] = 32 * i;
+  int ok = 0;
+  CK(sign_impl(ctx, sks32, msgs32, offs.data(), B, out96, &ok));
+  return ok;
+}
+
+static int sk_to_pk_impl(bls_ctx* ctx, const uint8_t* sks, size_t n, uint8_t* out48) {
+  uint8_t *d_sk, *d_out;
+  int* d_ok;
+  SCR(S_IN0, 32 * n, d_sk);
+  SCR(S_IN2, 48 * n, d_out);
+  SCR(S_OK, n, d_ok);
+  CK(h2d(ctx, d_sk, sks, 32 * n));
+  LK(launch_sk_to_pk_many(ctx->stream, d_sk, n, d_out, d_ok));
+  std::vector<int> ok(n);
+  CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
+  CK(d2h(ctx, out48, d_out, 48 * n));
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) return 0;
+  return 1;
+}
+
+int bls_sk_to_pk(bls_ctx* ctx, const uint8_t* sk32, uint8_t* out48) {
+  API_ENTER(ctx);
+  if (!sk32 || !out48) return BLS_E_ARG;
+  return sk_to_pk_impl(ctx, sk32, 1, out48);
+}
+
+int bls_sk_to_pk_batch(bls_ctx* ctx, const uint8_t* sks32, size_t B, uint8_t* out48) {
+  API_ENTER(ctx);
+  if ((!sks32 || !out48) && B) return BLS_E_ARG;
+  if (!B) return 1;
+  return sk_to_pk_impl(ctx, sks32, B, out48);
+}
+
+int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* dst, size_t dst_len,
+                   uint8_t* out96) {
+  API_ENTER(ctx);
+  if (!out96 || (!msg && msg_len) || !dst || dst_len == 0 || dst_len > 255 || msg_len > 0xffffffffu) return BLS_E_ARG;
+  uint8_t *d_m, *d_dst, *d_out;
+  uint64_t* d_offs;
+  G2A* h;
+  SCR(S_IN0, msg_len, d_m);
+  SCR(S_IN1, dst_len, d_dst);
+  SCR(S_IN2, 96, d_out);
+  SCR(S_OFFS, 2, d_offs);
+  SCR(S_G2A, 1, h);
+  uint64_t offs[2] = {0, msg_len};
+  CK(h2d(ctx, d_m, msg, msg_len));
+  CK(h2d(ctx, d_dst, dst, dst_len));
+  CK(h2d(ctx, d_offs, offs, sizeof offs));
+  LK(launch_hash_many(ctx->stream, d_m, d_offs, 1, d_dst, (uint32_t)dst_len, h));
+  LK(launch_g2_compress_aff(ctx->stream, h, d_out));
+  CK(d2h(ctx, out96, d_out, 96));
+  return 1;
+}
+
+// ------------------------------------------------------------- registry --
+int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid) {
+  API_ENTER(ctx);
+  if (!pks48 && n) return BLS_E_ARG;
+  if (n > 0xffffffffu) return BLS_E_ARG;
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  if (ctx->reg) HIPCK(hipFree(ctx->reg));
+  if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
+  ctx->reg = nullptr;
+  ctx->reg_ok = nullptr;
+  ctx->reg_n = 0;
+  HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(G1A)));
+  HIPCK(hipMalloc(&ctx->reg_ok, n ? n : 1));
+  uint8_t* d_in;
+  int* d_ok;
+  SCR(S_IN0, 48 * n, d_in);
+  SCR(S_OK, n, d_ok);
+  CK(h2d(ctx, d_in, pks48, 48 * n));
+  LK(launch_key_validate(ctx->stream, d_in, n, ctx->reg, d_ok));
+  LK(launch_status_to_u8(ctx->stream, d_ok, n, ctx->reg_ok));
+  if (out_valid) CK(d2h(ctx, out_valid, ctx->reg_ok, n));
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  ctx->reg_n = n;
+  return 1;
+}
+
+size_t bls_registry_size(bls_ctx* ctx) { return ctx ? ctx->reg_n : 0; }
+
+// ---------------------------------------------------------- FAV batches --
+static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offs, size_t B, const uint8_t* d_msgs,
+                       const uint8_t* d_sigs, const uint8_t* seed32, Fp12** out_f) {
+  if (!ctx->reg || !ctx->reg_n) {
+    ctx->err = "no registry loaded";
+    return BLS_E_NOREG;
+  }
+  G1J *apk;
+  int* status;
+  G1A *apka, *rP;
+  G2A *sig, *H;
+  G2J *rS, *tmp, *S;
+  Fp12 *f, *ft, *fo;
+  uint8_t* d_seed;
+  SCR(S_APK, B, apk);
+  SCR(S_STATUS, B + 1, status);
+  SCR(S_APKA, B, apka);
+  SCR(S_SIG, B, sig);
+  SCR(S_RP, B + 1, rP);
+  SCR(S_RS, B, rS);
+  SCR(S_H, B + 1, H);
+  SCR(S_G2J_T, 1024, tmp);
+  SCR(S_G2J, 1, S);
+  SCR(S_F, B + 1, f);
+  SCR(S_F_T, 512, ft);
+  SCR(S_FPART, 1, fo);
+  SCR(S_SEED, 32, d_seed);
+  CK(h2d(ctx, d_seed, seed32, 32));
+  hipStream_t st = ctx->stream;
+  LK(launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
+  LK(launch_fav_sig(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rP, rS));
+  LK(launch_fav_hash(st, B, d_msgs, status, H));
+  LK(launch_g2_sum_jac(st, rS, B, tmp, S));
+  LK(launch_sig_pair(st, S, rP + B, H + B));
+  HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));
+  LK(launch_miller(st, rP, H, status, B + 1, f));
+  LK(launch_fp12_prod(st, f, B + 1, ft, fo));
+  ctx->fav_B = B;
+  ctx->fav_ready = true;
+  *out_f = fo;
+  return 0;
+}
+
+static int fav_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
+  if (!ctx->fav_ready) {
+    ctx->err = "no prepared FAV batch";
+    return BLS_E_ARG;
+  }
+  size_t B = ctx->fav_B;
+  int* status = (int*)ctx->buf[S_STATUS].p;
+  if (batch_ok) {
+    LK(launch_status_to_u8(ctx->stream, status, B, d_out));
+  } else {
+    LK(launch_fav_single(ctx->stream, B, (G1A*)ctx->buf[S_APKA].p, (G2A*)ctx->buf[S_H].p, (G2A*)ctx->buf[S_SIG].p,
+                         status, d_out));
+  }
+  return 0;
+}
+
+static void host_seed(uint8_t seed[32]) {
+  // RLC scalars must be unpredictable to whoever produced the signatures.
+  FILE* f = fopen("/dev/urandom", "rb");
+  size_t got = f ? fread(seed, 1, 32, f) : 0;
+  if (f) fclose(f);
+  for (size_t i = got; i < 32; i++) seed[i] = (uint8_t)(i * 131 + 7);
+}
+
+int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* offsets, size_t B, const uint8_t* msgs32,
+                          const uint8_t* sigs96, uint8_t* out) {
+  API_ENTER(ctx);
+  if ((!offsets || !msgs32 || !sigs96 || !out) && B) return BLS_E_ARG;
+  if (!B) return 1;
+  const uint64_t nidx = offsets[B];
+  if (nidx && !idx) return BLS_E_ARG;
+  for (size_t b = 0; b < B; b++)
+    if (offsets[b + 1] < offsets[b]) return BLS_E_ARG;
+  uint32_t* d_idx;
+  uint64_t* d_offs;
+  uint8_t *d_m, *d_s, *d_out;
+  SCR(S_IN0, nidx, d_idx);
+  SCR(S_OFFS, B + 1, d_offs);
+  SCR(S_IN1, 32 * B, d_m);
+  SCR(S_IN2, 96 * B, d_s);
+  SCR(S_IN3, B, d_out);
+  CK(h2d(ctx, d_idx, idx, nidx * 4));
+  CK(h2d(ctx, d_offs, offsets, (B + 1) * 8));
+  CK(h2d(ctx, d_m, msgs32, 32 * B));
+  CK(h2d(ctx, d_s, sigs96, 96 * B));
+  uint8_t seed[32];
+  host_seed(seed);
+  Fp12* f;
+  CK(fav_prepare(ctx, d_idx, d_offs, B, d_m, d_s, seed, &f));
+  int ok = run_final_check(ctx, f);
+  if (ok < 0) return ok;
+  CK(fav_finish(ctx, ok, d_out));
+  CK(d2h(ctx, out, d_out, B));
+  return 1;
+}
+
+int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
+                             uint8_t* out) {
+  API_ENTER(ctx);
+  if ((!idx || !msgs32 || !sigs96 || !out) && B) return BLS_E_ARG;
+  if (!B) return 1;
+  if (!ctx->reg || !ctx->reg_n) {
+    ctx->err = "no registry loaded";
+    return BLS_E_NOREG;
+  }
+  uint32_t* d_idx;
+  uint8_t *d_m, *d_s, *d_out;
+  SCR(S_IN0, B, d_idx);
+  SCR(S_IN1, 32 * B, d_m);
+  SCR(S_IN2, 96 * B, d_s);
+  SCR(S_IN3, B, d_out);
+  CK(h2d(ctx, d_idx, idx, B * 4));
+  CK(h2d(ctx, d_m, msgs32, 32 * B));
+  CK(h2d(ctx, d_s, sigs96, 96 * B));
+  LK(launch_verify_indexed(ctx->stream, d_idx, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, d_m, d_s, d_out));
+  CK(d2h(ctx, out, d_out, B));
+  return 1;
+}
+
+// ------------------------------------------------------ device-resident --
+void* bls_dev_alloc(bls_ctx* ctx, size_t bytes) {
+  if (!ctx) return nullptr;
+  std::lock_guard<std::mutex> lock_(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+  return p;
+}
+
+int bls_dev_free(bls_ctx* ctx, void* p) {
+  API_ENTER(ctx);
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipFree(p));
+  return 0;
+}
+
+int bls_h2d(bls_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  API_ENTER(ctx);
+  CK(h2d(ctx, dst, src, bytes));
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int bls_d2h(bls_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  API_ENTER(ctx);
+  CK(d2h(ctx, dst, src, bytes));
+  return 0;
+}
+
+int bls_sync(bls_ctx* ctx) {
+  API_ENTER(ctx);
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
+                              const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32,
+                              uint8_t* partial576) {
+  API_ENTER(ctx);
+  if (!d_offsets || !d_msgs32 || !d_sigs96 || !seed32 || !partial576 || !B) return BLS_E_ARG;
+  Fp12* f;
+  CK(fav_prepare(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32, &f));
+  uint8_t* d_b;
+  SCR(S_BYTES, 576, d_b);
+  LK(launch_fp12_to_bytes(ctx->stream, f, d_b));
+  CK(d2h(ctx, partial576, d_b, 576));
+  return 1;
+}
+
+int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
+  API_ENTER(ctx);
+  if (!partials576 || !n) return BLS_E_ARG;
+  uint8_t* d_b;
+  Fp12 *f, *ft;
+  SCR(S_IN0, 576 * n, d_b);
+  SCR(S_F_T, 512 + n, f);
+  Fp12* fbase = f;
+  ft = fbase + n;
+  Fp12* out;
+  SCR(S_FCHK, 1, out);
+  CK(h2d(ctx, d_b, partials576, 576 * n));
+  LK(launch_fp12_from_bytes(ctx->stream, d_b, n, fbase));
+  LK(launch_fp12_prod(ctx->stream, fbase, n, ft, out));
+  return run_final_check(ctx, out);
+}
+
+int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
+  API_ENTER(ctx);
+  if (!d_out) return BLS_E_ARG;
+  CK(fav_finish(ctx, batch_ok, d_out));
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  return 1;
+}
+
+}  // extern "C"

@@ -10,7 +10,7 @@
 #include <stdint.h>
 
 #define BLS_HD __host__ __device__ __forceinline__
-#define BLS_HDNI __host__ __device__ __noinline__
+#define BLS_HDNI __host__ __device__ inline __attribute__((noinline))
 
 namespace bls {
 

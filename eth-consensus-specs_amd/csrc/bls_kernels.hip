@@ -1,0 +1,505 @@
+// gfx950 kernels of the BLS12-381 backend.  One lane owns one item
+// (verification, key, signature, pair) unless noted; reductions (aggregate
+// pubkeys, sum of r_i*sig_i, Miller-product) are LDS trees inside a
+// workgroup followed by a second pass over the per-workgroup partials.
+#include "bls_kernels.h"
+
+namespace bls {
+
+__device__ static const uint8_t DST_POP_DEV[43] = {
+    'B', 'L', 'S', '_', 'S', 'I', 'G', '_', 'B', 'L', 'S', '1', '2', '3', '8', '1', 'G', '2', '_', 'X', 'M', 'D',
+    ':', 'S', 'H', 'A', '-', '2', '5', '6', '_', 'S', 'S', 'W', 'U', '_', 'R', 'O', '_', 'P', 'O', 'P', '_'};
+
+static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+// ---------------------------------------------------------------- decode --
+__global__ void __launch_bounds__(64) k_key_validate(const uint8_t* pks48, size_t n, G1A* out, int* ok) {
+  size_t i = gtid();
+  if (i >= n) return;
+  G1A a;
+  int v = key_validate(a, pks48 + 48 * i);
+  if (!v) a = G1A{fp_zero(), fp_zero(), true};
+  out[i] = a;
+  ok[i] = v;
+}
+
+__global__ void __launch_bounds__(64) k_sig_validate(const uint8_t* sigs96, size_t n, G2A* out, int* ok) {
+  size_t i = gtid();
+  if (i >= n) return;
+  G2A a;
+  int v = sig_validate(a, sigs96 + 96 * i);
+  if (!v) a = G2A{fp2_zero(), fp2_zero(), true};
+  out[i] = a;
+  ok[i] = v;
+}
+
+// ------------------------------------------------------------ reductions --
+// Sum of affine G1 points (only entries with ok != 0 when ok is given) into
+// one Jacobian partial per workgroup.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_g1_sum_aff(const G1A* in, const int* ok, size_t n, G1J* out) {
+  __shared__ G1J sh[NT];
+  G1J acc = jac_identity<Fp>();
+  for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < n; i += (size_t)gridDim.x * NT) {
+    if (!ok || ok[i]) acc = jac_add_aff(acc, in[i]);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] = jac_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+
+template <class F, int NT>
+__global__ void __launch_bounds__(NT) k_jac_sum(const Jac<F>* in, size_t n, Jac<F>* out) {
+  __shared__ Jac<F> sh[NT];
+  Jac<F> acc = jac_identity<F>();
+  for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < n; i += (size_t)gridDim.x * NT) acc = jac_add(acc, in[i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] = jac_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(64) k_g2_sum_aff(const G2A* in, const int* ok, size_t n, G2J* out) {
+  __shared__ G2J sh[64];
+  G2J acc = jac_identity<Fp2>();
+  for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (size_t)gridDim.x * 64) {
+    if (!ok || ok[i]) acc = jac_add(acc, jac_from_aff(in[i]));
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] = jac_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(64) k_fp12_prod(const Fp12* in, size_t n, Fp12* out) {
+  __shared__ Fp12 sh[64];
+  Fp12 acc = fp12_one();
+  for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (size_t)gridDim.x * 64) acc = fp12_mul(acc, in[i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] = fp12_mul(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+
+// ------------------------------------------------------------- encoding --
+__global__ void k_g1_compress(const G1J* in, uint8_t* out48, int* is_inf) {
+  if (threadIdx.x || blockIdx.x) return;
+  G1A a = jac_to_aff(in[0]);
+  g1_compress(out48, a);
+  if (is_inf) *is_inf = a.inf;
+}
+
+__global__ void k_g2_compress(const G2J* in, uint8_t* out96) {
+  if (threadIdx.x || blockIdx.x) return;
+  g2_compress(out96, jac_to_aff(in[0]));
+}
+
+// ------------------------------------------------------------ per-call ---
+__global__ void k_verify_single(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
+                                int* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  G1A pk;
+  if (!key_validate(pk, pk48)) {
+    *out = 0;
+    return;
+  }
+  *out = core_verify_point(pk, msg, msg_len, DST_POP_DEV, 43, sig96);
+}
+
+// CoreVerify on an aggregate (Jacobian) public key; identity -> invalid.
+__global__ void k_verify_apk(const G1J* apk, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96, int* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  G1A a = jac_to_aff(apk[0]);
+  if (a.inf) {
+    *out = 0;
+    return;
+  }
+  *out = core_verify_point(a, msg, msg_len, DST_POP_DEV, 43, sig96);
+}
+
+__global__ void __launch_bounds__(64) k_hash_many(const uint8_t* msgs, const uint64_t* offs, size_t n,
+                                                  const uint8_t* dst, uint32_t dst_len, G2A* out) {
+  size_t i = gtid();
+  if (i >= n) return;
+  const uint8_t* d = dst ? dst : DST_POP_DEV;
+  uint32_t dl = dst ? dst_len : 43;
+  out[i] = jac_to_aff(hash_to_g2(msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), d, dl));
+}
+
+__global__ void __launch_bounds__(64) k_miller(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
+  size_t i = gtid();
+  if (i >= n) return;
+  f[i] = (!ok || ok[i]) ? miller_loop(P[i], Q[i]) : fp12_one();
+}
+
+__global__ void k_final_check(const Fp12* f, int* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  *out = fp12_is_one(final_exponentiation(f[0])) ? 1 : 0;
+}
+
+__global__ void k_g2_compress_aff(const G2A* in, uint8_t* out96) {
+  if (threadIdx.x || blockIdx.x) return;
+  g2_compress(out96, in[0]);
+}
+
+// --------------------------------------------------------------- signing --
+// sk: 32 bytes big-endian -> 8 LE u32 limbs; valid iff 0 < sk < r
+static __device__ bool sk_parse(uint32_t k[8], const uint8_t* sk) {
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = sk + 28 - 4 * i;
+    k[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+  static constexpr uint32_t R_LIMBS[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                          0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  uint32_t nz = 0;
+  for (int i = 0; i < 8; i++) nz |= k[i];
+  if (!nz) return false;
+  for (int i = 7; i >= 0; --i) {
+    if (k[i] != R_LIMBS[i]) return k[i] < R_LIMBS[i];
+  }
+  return false;  // == r
+}
+
+__global__ void __launch_bounds__(64) k_sign_many(const uint8_t* sks32, const uint8_t* msgs, const uint64_t* offs,
+                                                  size_t n, uint8_t* out96, int* ok) {
+  size_t i = gtid();
+  if (i >= n) return;
+  uint32_t k[8];
+  if (!sk_parse(k, sks32 + 32 * i)) {
+    ok[i] = 0;
+    return;
+  }
+  G2J h = hash_to_g2(msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_DEV, 43);
+  g2_compress(out96 + 96 * i, jac_to_aff(jac_mul_u256(h, k)));
+  ok[i] = 1;
+}
+
+__global__ void __launch_bounds__(64) k_sk_to_pk_many(const uint8_t* sks32, size_t n, uint8_t* out48, int* ok) {
+  size_t i = gtid();
+  if (i >= n) return;
+  uint32_t k[8];
+  if (!sk_parse(k, sks32 + 32 * i)) {
+    ok[i] = 0;
+    return;
+  }
+  g1_compress(out48 + 48 * i, jac_to_aff(jac_mul_u256(jac_from_aff(g1_generator()), k)));
+  ok[i] = 1;
+}
+
+// ------------------------------------------------------- FAV batch path --
+// (1) aggregate pubkeys: one 64-lane workgroup per item, strided mixed
+//     additions from the HBM registry, then an LDS tree.
+__global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
+                                                   const uint8_t* reg_ok, uint32_t reg_n, G1J* apk, int* status) {
+  __shared__ G1J sh[64];
+  __shared__ int bad;
+  const size_t b = blockIdx.x;
+  if (b >= B) return;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const uint64_t lo = offs[b], hi = offs[b + 1];
+  G1J acc = jac_identity<Fp>();
+  int mybad = 0;
+  for (uint64_t j = lo + threadIdx.x; j < hi; j += 64) {
+    uint32_t k = idx[j];
+    if (k >= reg_n || !reg_ok[k]) {
+      mybad = 1;
+    } else {
+      acc = jac_add_aff(acc, reg[k]);
+    }
+  }
+  if (mybad) atomicOr(&bad, 1);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] = jac_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    apk[b] = sh[0];
+    status[b] = (hi > lo && !bad) ? 1 : 0;
+  }
+}
+
+// RLC scalar r_i = first 8 bytes of SHA-256(seed || i || msg || sig), nonzero.
+static __device__ uint64_t rlc_scalar(const uint8_t* seed32, uint64_t i, const uint8_t* msg32, const uint8_t* sig96) {
+  Sha256 s;
+  sha256_init(s);
+  sha256_update(s, seed32, 32);
+  for (int k = 0; k < 8; k++) sha256_byte(s, (uint8_t)(i >> (8 * k)));
+  sha256_update(s, msg32, 32);
+  sha256_update(s, sig96, 96);
+  uint8_t d[32];
+  sha256_final(s, d);
+  uint64_t r = 0;
+  for (int k = 0; k < 8; k++) r = (r << 8) | d[k];
+  return r ? r : 1;
+}
+
+// (2a) per item: signature decode + subgroup check, apk affine, RLC scalars.
+__global__ void __launch_bounds__(64) k_fav_sig(size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
+                                                const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff,
+                                                G2A* sig, G1A* rP, G2J* rS) {
+  size_t i = gtid();
+  if (i >= B) return;
+  G1A a{fp_zero(), fp_zero(), true};
+  G2A s{fp2_zero(), fp2_zero(), true};
+  int st = status[i];
+  if (st) {
+    a = jac_to_aff(apk[i]);
+    if (a.inf) st = 0;
+  }
+  if (st && !sig_validate(s, sigs96 + 96 * i)) st = 0;
+  if (st) {
+    uint64_t r = rlc_scalar(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i);
+    rP[i] = jac_to_aff(jac_mul_u64(jac_from_aff(a), r));
+    rS[i] = jac_mul_u64(jac_from_aff(s), r);
+  } else {
+    rP[i] = G1A{fp_zero(), fp_zero(), true};
+    rS[i] = jac_identity<Fp2>();
+  }
+  apk_aff[i] = a;
+  sig[i] = s;
+  status[i] = st;
+}
+
+// (2b) per item: hash_to_G2 of the 32-byte signing root.
+__global__ void __launch_bounds__(64) k_fav_hash(size_t B, const uint8_t* msgs32, const int* status, G2A* H) {
+  size_t i = gtid();
+  if (i >= B) return;
+  if (!status[i]) {
+    H[i] = G2A{fp2_zero(), fp2_zero(), true};
+    return;
+  }
+  H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_DEV, 43));
+}
+
+// Affine conversion of the summed signature side, negated generator pair.
+__global__ void k_sig_pair(const G2J* S, G1A* P, G2A* Q) {
+  if (threadIdx.x || blockIdx.x) return;
+  *Q = jac_to_aff(S[0]);
+  G1A g = g1_generator();
+  g.y = fp_neg(g.y);
+  *P = g;
+}
+
+// (4) fallback: individual checks e(apk_i, H_i) e(-G1, sig_i) == 1
+__global__ void __launch_bounds__(64) k_fav_single(size_t B, const G1A* apk_aff, const G2A* H, const G2A* sig,
+                                                   const int* status, uint8_t* out) {
+  size_t i = gtid();
+  if (i >= B) return;
+  if (!status[i]) {
+    out[i] = 0;
+    return;
+  }
+  G1A g = g1_generator();
+  g.y = fp_neg(g.y);
+  out[i] = pairing_check2(apk_aff[i], H[i], g, sig[i]) ? 1 : 0;
+}
+
+__global__ void k_status_to_u8(const int* status, size_t B, uint8_t* out) {
+  size_t i = gtid();
+  if (i < B) out[i] = status[i] ? 1 : 0;
+}
+
+// Gossip: registry-indexed single Verify per lane (no batching across items).
+__global__ void __launch_bounds__(64) k_verify_indexed(const uint32_t* idx, size_t B, const G1A* reg,
+                                                       const uint8_t* reg_ok, uint32_t reg_n, const uint8_t* msgs32,
+                                                       const uint8_t* sigs96, uint8_t* out) {
+  size_t i = gtid();
+  if (i >= B) return;
+  uint32_t k = idx[i];
+  if (k >= reg_n || !reg_ok[k]) {
+    out[i] = 0;
+    return;
+  }
+  out[i] = core_verify_point(reg[k], msgs32 + 32 * i, 32, DST_POP_DEV, 43, sigs96 + 96 * i) ? 1 : 0;
+}
+
+// Fp12 <-> 576 big-endian bytes (w-basis order c0..c5, each Fp2 as c0||c1)
+__global__ void k_fp12_to_bytes(const Fp12* f, uint8_t* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  const Fp2* c[6] = {&f->c0.c0, &f->c1.c0, &f->c0.c1, &f->c1.c1, &f->c0.c2, &f->c1.c2};
+  for (int k = 0; k < 6; k++) {
+    raw_to_be48(fp_from_mont(c[k]->c0), out + 96 * k);
+    raw_to_be48(fp_from_mont(c[k]->c1), out + 96 * k + 48);
+  }
+}
+
+__global__ void k_fp12_from_bytes(const uint8_t* in, size_t n, Fp12* f) {
+  size_t i = gtid();
+  if (i >= n) return;
+  const uint8_t* b = in + 576 * i;
+  Fp12 r;
+  Fp2* c[6] = {&r.c0.c0, &r.c1.c0, &r.c0.c1, &r.c1.c1, &r.c0.c2, &r.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    c[k]->c0 = fp_to_mont(raw_from_be48(b + 96 * k));
+    c[k]->c1 = fp_to_mont(raw_from_be48(b + 96 * k + 48));
+  }
+  f[i] = r;
+}
+
+// ======================================================= host launchers ==
+static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+#define LAUNCH(k, g, b, st, ...)                              \
+  do {                                                        \
+    hipLaunchKernelGGL(k, dim3(g), dim3(b), 0, st, __VA_ARGS__); \
+    hipError_t e__ = hipGetLastError();                       \
+    if (e__ != hipSuccess) return e__;                        \
+  } while (0)
+
+hipError_t launch_key_validate(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_key_validate, nblk(n, 64), 64, st, pks, n, out, ok);
+  return hipSuccess;
+}
+hipError_t launch_sig_validate(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_sig_validate, nblk(n, 64), 64, st, sigs, n, out, ok);
+  return hipSuccess;
+}
+
+// Two-pass sums; tmp must hold >= 1 + nblk entries.
+hipError_t launch_g1_sum_aff(hipStream_t st, const G1A* in, const int* ok, size_t n, G1J* tmp, G1J* out) {
+  unsigned g = nblk(n, 64);
+  if (g > 1024) g = 1024;
+  if (g == 0) g = 1;
+  LAUNCH((k_g1_sum_aff<64>), g, 64, st, in, ok, n, tmp);
+  LAUNCH((k_jac_sum<Fp, 64>), 1, 64, st, tmp, (size_t)g, out);
+  return hipSuccess;
+}
+hipError_t launch_g2_sum_aff(hipStream_t st, const G2A* in, const int* ok, size_t n, G2J* tmp, G2J* out) {
+  unsigned g = nblk(n, 64);
+  if (g > 1024) g = 1024;
+  if (g == 0) g = 1;
+  LAUNCH(k_g2_sum_aff, g, 64, st, in, ok, n, tmp);
+  LAUNCH((k_jac_sum<Fp2, 64>), 1, 64, st, tmp, (size_t)g, out);
+  return hipSuccess;
+}
+hipError_t launch_g2_sum_jac(hipStream_t st, const G2J* in, size_t n, G2J* tmp, G2J* out) {
+  unsigned g = nblk(n, 64);
+  if (g > 1024) g = 1024;
+  if (g == 0) g = 1;
+  LAUNCH((k_jac_sum<Fp2, 64>), g, 64, st, in, n, tmp);
+  LAUNCH((k_jac_sum<Fp2, 64>), 1, 64, st, tmp, (size_t)g, out);
+  return hipSuccess;
+}
+hipError_t launch_fp12_prod(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out) {
+  unsigned g = nblk(n, 64);
+  if (g > 512) g = 512;
+  if (g == 0) g = 1;
+  LAUNCH(k_fp12_prod, g, 64, st, in, n, tmp);
+  LAUNCH(k_fp12_prod, 1, 64, st, tmp, (size_t)g, out);
+  return hipSuccess;
+}
+hipError_t launch_g1_compress(hipStream_t st, const G1J* in, uint8_t* out48, int* is_inf) {
+  LAUNCH(k_g1_compress, 1, 64, st, in, out48, is_inf);
+  return hipSuccess;
+}
+hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96) {
+  LAUNCH(k_g2_compress, 1, 64, st, in, out96);
+  return hipSuccess;
+}
+hipError_t launch_verify_single(hipStream_t st, const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig,
+                                int* out) {
+  LAUNCH(k_verify_single, 1, 64, st, pk, msg, len, sig, out);
+  return hipSuccess;
+}
+hipError_t launch_verify_apk(hipStream_t st, const G1J* apk, const uint8_t* msg, uint32_t len, const uint8_t* sig,
+                             int* out) {
+  LAUNCH(k_verify_apk, 1, 64, st, apk, msg, len, sig, out);
+  return hipSuccess;
+}
+hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst,
+                            uint32_t dst_len, G2A* out) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_hash_many, nblk(n, 64), 64, st, msgs, offs, n, dst, dst_len, out);
+  return hipSuccess;
+}
+hipError_t launch_miller(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_miller, nblk(n, 64), 64, st, P, Q, ok, n, f);
+  return hipSuccess;
+}
+hipError_t launch_final_check(hipStream_t st, const Fp12* f, int* out) {
+  LAUNCH(k_final_check, 1, 64, st, f, out);
+  return hipSuccess;
+}
+hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n,
+                            uint8_t* out, int* ok) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_sign_many, nblk(n, 64), 64, st, sks, msgs, offs, n, out, ok);
+  return hipSuccess;
+}
+hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_sk_to_pk_many, nblk(n, 64), 64, st, sks, n, out, ok);
+  return hipSuccess;
+}
+hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
+                             const uint8_t* reg_ok, uint32_t reg_n, G1J* apk, int* status) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_fav_gather, (unsigned)B, 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+  return hipSuccess;
+}
+hipError_t launch_fav_sig(hipStream_t st, size_t B, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* seed,
+                          const G1J* apk, int* status, G1A* apk_aff, G2A* sig, G1A* rP, G2J* rS) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_fav_sig, nblk(B, 64), 64, st, B, msgs, sigs, seed, apk, status, apk_aff, sig, rP, rS);
+  return hipSuccess;
+}
+hipError_t launch_fav_hash(hipStream_t st, size_t B, const uint8_t* msgs, const int* status, G2A* H) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_fav_hash, nblk(B, 64), 64, st, B, msgs, status, H);
+  return hipSuccess;
+}
+hipError_t launch_sig_pair(hipStream_t st, const G2J* S, G1A* P, G2A* Q) {
+  LAUNCH(k_sig_pair, 1, 64, st, S, P, Q);
+  return hipSuccess;
+}
+hipError_t launch_fav_single(hipStream_t st, size_t B, const G1A* apk_aff, const G2A* H, const G2A* sig,
+                             const int* status, uint8_t* out) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_fav_single, nblk(B, 64), 64, st, B, apk_aff, H, sig, status, out);
+  return hipSuccess;
+}
+hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_status_to_u8, nblk(B, 256), 256, st, status, B, out);
+  return hipSuccess;
+}
+hipError_t launch_verify_indexed(hipStream_t st, const uint32_t* idx, size_t B, const G1A* reg, const uint8_t* reg_ok,
+                                 uint32_t reg_n, const uint8_t* msgs, const uint8_t* sigs, uint8_t* out) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_verify_indexed, nblk(B, 64), 64, st, idx, B, reg, reg_ok, reg_n, msgs, sigs, out);
+  return hipSuccess;
+}
+hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out) {
+  LAUNCH(k_fp12_to_bytes, 1, 64, st, f, out);
+  return hipSuccess;
+}
+hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, Fp12* f) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_fp12_from_bytes, nblk(n, 64), 64, st, in, n, f);
+  return hipSuccess;
+}
+hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96) {
+  LAUNCH(k_g2_compress_aff, 1, 64, st, in, out96);
+  return hipSuccess;
+}
+
+}  // namespace bls

@@ -1,0 +1,131 @@
+/*
+ * libblsmi355x -- MI355X (gfx950) BLS12-381 signature-verification backend.
+ *
+ * C ABI: plain pointers and sizes, caller-owned contiguous buffers, no torch
+ * or HIP types.  It replaces the arithmetic the reference reaches through
+ * ``eth2spec.utils.bls`` (reference ``tests/core/pyspec/eth2spec/utils/bls.py``,
+ * written ``E/utils/bls.py`` below), i.e. the milagro_bls_binding /
+ * py_ecc entry points bound at E/utils/bls.py:1-32,57-68.
+ *
+ * Return convention:
+ *    1  valid / success
+ *    0  invalid input (decode, subgroup, infinity, empty-list rejection,
+ *       failed verification)
+ *   <0  internal or device error (BLS_E_*); bls_last_error() describes it.
+ * The Python shim maps a negative code to an exception everywhere, and 0 to
+ * an exception exactly where the reference raises (Aggregate, AggregatePKs,
+ * Sign, SkToPk), to False elsewhere.
+ *
+ * Threading: one context per process/device; calls on a context are
+ * serialised by an internal mutex.  All device memory and streams are owned
+ * by the context.  Every compute entry point runs on the GPU; there is no
+ * CPU fallback (a missing/failed device is an error).
+ */
+#ifndef BLSMI355X_H
+#define BLSMI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLS_E_DEVICE (-1)  /* HIP runtime / kernel failure */
+#define BLS_E_ARG (-2)     /* bad argument (NULL pointer, size overflow) */
+#define BLS_E_NOREG (-3)   /* indexed call without a loaded registry */
+
+typedef struct bls_ctx bls_ctx;
+
+/* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
+int bls_ctx_create(int device, bls_ctx** out);
+void bls_ctx_destroy(bls_ctx* ctx);
+const char* bls_last_error(bls_ctx* ctx);
+/* Device name / CU count for reports; returns 0 or BLS_E_*. */
+int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count);
+
+/* ---- drop-in per-call API (one call = one reference wrapper call) ---- */
+
+/* Verify  <- E/utils/bls.py:141-151 (milagro Verify / py_ecc Verify). */
+int bls_verify(bls_ctx* ctx, const uint8_t* pk48, const uint8_t* msg, size_t msg_len, const uint8_t* sig96);
+
+/* FastAggregateVerify  <- E/utils/bls.py:167-177.  n == 0 -> 0. */
+int bls_fast_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
+                              const uint8_t* sig96);
+
+/* AggregateVerify  <- E/utils/bls.py:154-164.  msgs is the concatenation of
+ * the n messages, msg_lens[i] their lengths.  n == 0 -> 0. */
+int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msgs, const size_t* msg_lens,
+                         const uint8_t* sig96);
+
+/* Aggregate  <- E/utils/bls.py:180-184.  1 and out96 on success; 0 on empty
+ * list or an undecodable / non-G2 signature (the reference raises). */
+int bls_aggregate(bls_ctx* ctx, const uint8_t* sigs96, size_t n, uint8_t* out96);
+
+/* _AggregatePKs  <- E/utils/bls.py:202-213 (eth_aggregate_pubkeys,
+ * specs/altair/bls.md:36-52).  0 on empty list or any key failing
+ * KeyValidate (the reference raises). */
+int bls_aggregate_pks(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out48);
+
+/* KeyValidate  <- E/utils/bls.py:395-397. */
+int bls_key_validate(bls_ctx* ctx, const uint8_t* pk48);
+
+/* Sign / SkToPk  <- E/utils/bls.py:187-194,216-221; sk is 32 bytes
+ * big-endian, 0 < sk < r (else 0). */
+int bls_sign(bls_ctx* ctx, const uint8_t* sk32, const uint8_t* msg, size_t msg_len, uint8_t* out96);
+int bls_sk_to_pk(bls_ctx* ctx, const uint8_t* sk32, uint8_t* out48);
+
+/* hash_to_G2 (RFC 9380 BLS12381G2_XMD:SHA-256_SSWU_RO_) with caller DST,
+ * compressed output.  The POP DST is the spec's (beacon-chain.md:692). */
+int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* dst, size_t dst_len,
+                   uint8_t* out96);
+
+/* ---- batch API (throughput path) -------------------- */
+
+/* Decode + KeyValidate n compressed pubkeys into the HBM-resident affine
+ * registry (replacing any previous one).  out_valid[i] = 1/0 (may be NULL).
+ * Returns 1 or BLS_E_*. */
+int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid);
+size_t bls_registry_size(bls_ctx* ctx);
+
+/* B FastAggregateVerify calls over registry indices: item b uses
+ * idx[offsets[b] .. offsets[b+1]) (offsets has B+1 entries), message
+ * msgs32[32 b ..], signature sigs96[96 b ..].  out[b] = 1/0.  One random-
+ * linear-combination pairing check for the whole batch, per-item fallback
+ * on failure.  Returns 1 or BLS_E_*. */
+int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* offsets, size_t B, const uint8_t* msgs32,
+                          const uint8_t* sigs96, uint8_t* out);
+
+/* B independent Verify calls with registry indices (gossip firehose). */
+int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const uint8_t* msgs32,
+                             const uint8_t* sigs96, uint8_t* out);
+
+/* Synthetic-data helpers (used by bench.py and tests to make inputs). */
+int bls_sign_batch(bls_ctx* ctx, const uint8_t* sks32, const uint8_t* msgs32, size_t B, uint8_t* out96);
+int bls_sk_to_pk_batch(bls_ctx* ctx, const uint8_t* sks32, size_t B, uint8_t* out48);
+
+/* ---- device-resident variants (inputs already in HBM) ----------------- */
+void* bls_dev_alloc(bls_ctx* ctx, size_t bytes);
+int bls_dev_free(bls_ctx* ctx, void* dptr);
+int bls_h2d(bls_ctx* ctx, void* dst, const void* src, size_t bytes);
+int bls_d2h(bls_ctx* ctx, void* dst, const void* src, size_t bytes);
+int bls_sync(bls_ctx* ctx);
+
+/* Phase 1 of a (possibly multi-GPU) FAV batch on device pointers: per-item
+ * checks and this shard's Miller-loop product, written to partial576 (host,
+ * 576 bytes: 12 Fp2 coefficients, big-endian).  d_status (device, B ints)
+ * receives the per-item pre-pairing validity.  seed32 keys the RLC scalars. */
+int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
+                              const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32,
+                              uint8_t* partial576);
+/* Final exponentiation of the product of n partials == 1 ?  1 / 0. */
+int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n);
+/* Phase 2: write verdicts for the batch prepared by the last
+ * bls_fav_batch_partial_dev call on this context.  batch_ok = result of
+ * bls_partials_check; when 0 every item is re-checked individually. */
+int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLSMI355X_H */
