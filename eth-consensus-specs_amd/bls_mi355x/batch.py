@@ -43,6 +43,13 @@ class Registry:
         c.check(c.lib.bls_registry_load(c.h, buf.tobytes(), n, _ptr(valid)))
         return valid
 
+    def generate(self, n: int, first_sk: int = 1, want_bytes: bool = False):
+        """Synthetic registry pk_i = (first_sk + i)*G1 built on the device (benchmarks)."""
+        c = self.ctx
+        out = ctypes.create_string_buffer(48 * n) if want_bytes else None
+        c.check(c.lib.bls_registry_generate(c.h, first_sk, n, out))
+        return out.raw if want_bytes else None
+
     def __len__(self):
         return int(self.ctx.lib.bls_registry_size(self.ctx.h))
 
@@ -169,3 +176,23 @@ class ResidentFavBatch:
     def free(self):
         for b in (self.idx, self.offs, self.msgs, self.sigs, self.out):
             b.free()
+
+
+class Profiler:
+    """hipEvent timing of each kernel of the FAV path (C-ABI bls_profile_*)."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or _native.context()
+
+    def start(self):
+        self.ctx.check(self.ctx.lib.bls_profile_enable(self.ctx.h, 1))
+
+    def stop(self):
+        self.ctx.check(self.ctx.lib.bls_profile_enable(self.ctx.h, 0))
+
+    def read(self) -> dict:
+        c = self.ctx
+        ms = (ctypes.c_double * 16)()
+        cnt = (ctypes.c_uint64 * 16)()
+        n = c.check(c.lib.bls_profile_read(c.h, ms, cnt, 16))
+        return {c.lib.bls_profile_name(i).decode(): (ms[i], int(cnt[i])) for i in range(n)}

@@ -42,7 +42,17 @@ struct bls_ctx {
   // last prepared FAV batch
   size_t fav_B = 0;
   bool fav_ready = false;
+  // per-kernel hipEvent timing of the FAV path (bls_profile_*)
+  bool prof_on = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_pool;
+  double prof_ms[16] = {0};
+  uint64_t prof_cnt[16] = {0};
 };
+
+static const char* const PROF_NAMES[] = {"fav_gather", "fav_sig", "fav_hash", "g2_sum", "sig_pair", "miller",
+                                         "fp12_prod", "final_exp", "fav_finish", "partials_prod"};
+static const int PROF_N = sizeof(PROF_NAMES) / sizeof(PROF_NAMES[0]);
 
 namespace {
 
@@ -126,10 +136,52 @@ int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** o
   return 1;
 }
 
+// Event pair around one launch when profiling is on.
+struct ProfScope {
+  bls_ctx* c;
+  int id;
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  ProfScope(bls_ctx* c_, int id_) : c(c_), id(id_) {
+    if (!c->prof_on) return;
+    if (c->prof_pool.empty()) {
+      hipEvent_t a, b;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+      c->prof_pool.push_back({a, b});
+    }
+    ev = c->prof_pool.back();
+    c->prof_pool.pop_back();
+    (void)hipEventRecord(ev.first, c->stream);
+  }
+  ~ProfScope() {
+    if (!ev.first) return;
+    (void)hipEventRecord(ev.second, c->stream);
+    c->prof_pending.push_back({id, ev});
+  }
+};
+
+void prof_collect(bls_ctx* c) {
+  for (auto& p : c->prof_pending) {
+    float ms = 0;
+    if (hipEventSynchronize(p.second.second) == hipSuccess &&
+        hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) {
+      c->prof_ms[p.first] += ms;
+      c->prof_cnt[p.first] += 1;
+    }
+    c->prof_pool.push_back(p.second);
+  }
+  c->prof_pending.clear();
+}
+
+#define PROF(id, expr)          \
+  do {                          \
+    ProfScope ps_(ctx, id);     \
+    LK(expr);                   \
+  } while (0)
+
 int run_final_check(bls_ctx* ctx, const Fp12* f) {
   int* d_r;
   SCR(S_INT, 4, d_r);
-  LK(launch_final_check(ctx->stream, f, d_r));
+  PROF(7, launch_final_check(ctx->stream, f, d_r));
   int r = 0;
   CK(d2h(ctx, &r, d_r, sizeof r));
   return r ? 1 : 0;
@@ -174,6 +226,11 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (auto& b : ctx->buf)
     if (b.p) (void)hipFree(b.p);
+  for (auto& p : ctx->prof_pending) ctx->prof_pool.push_back(p.second);
+  for (auto& p : ctx->prof_pool) {
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
   if (ctx->reg) (void)hipFree(ctx->reg);
   if (ctx->reg_ok) (void)hipFree(ctx->reg_ok);
   (void)hipStreamDestroy(ctx->stream);
@@ -453,6 +510,54 @@ int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out
 
 size_t bls_registry_size(bls_ctx* ctx) { return ctx ? ctx->reg_n : 0; }
 
+int bls_registry_generate(bls_ctx* ctx, uint64_t first_sk, size_t n, uint8_t* out_pks48) {
+  API_ENTER(ctx);
+  if (n > 0xffffffffu || first_sk == 0 || first_sk + n < first_sk || first_sk + n >= (1ull << 62)) return BLS_E_ARG;
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  if (ctx->reg) HIPCK(hipFree(ctx->reg));
+  if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
+  ctx->reg = nullptr;
+  ctx->reg_ok = nullptr;
+  ctx->reg_n = 0;
+  HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(G1A)));
+  HIPCK(hipMalloc(&ctx->reg_ok, n ? n : 1));
+  G1J* tmp;
+  uint8_t* d_out = nullptr;
+  SCR(S_G1J_T, n, tmp);
+  if (out_pks48) SCR(S_IN0, 48 * n, d_out);
+  LK(launch_registry_generate(ctx->stream, first_sk, n, tmp, ctx->reg, ctx->reg_ok, d_out));
+  if (out_pks48) CK(d2h(ctx, out_pks48, d_out, 48 * n));
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  ctx->reg_n = n;
+  return 1;
+}
+
+int bls_profile_enable(bls_ctx* ctx, int on) {
+  API_ENTER(ctx);
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  prof_collect(ctx);
+  ctx->prof_on = on != 0;
+  for (int i = 0; i < 16; i++) {
+    ctx->prof_ms[i] = 0;
+    ctx->prof_cnt[i] = 0;
+  }
+  return 0;
+}
+
+int bls_profile_read(bls_ctx* ctx, double* total_ms, uint64_t* counts, int max) {
+  API_ENTER(ctx);
+  HIPCK(hipStreamSynchronize(ctx->stream));
+  prof_collect(ctx);
+  int n = max < PROF_N ? max : PROF_N;
+  for (int i = 0; i < n; i++) {
+    if (total_ms) total_ms[i] = ctx->prof_ms[i];
+    if (counts) counts[i] = ctx->prof_cnt[i];
+  }
+  return PROF_N;
+}
+
+const char* bls_profile_name(int i) { return (i >= 0 && i < PROF_N) ? PROF_NAMES[i] : ""; }
+
 // ---------------------------------------------------------- FAV batches --
 static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offs, size_t B, const uint8_t* d_msgs,
                        const uint8_t* d_sigs, const uint8_t* seed32, Fp12** out_f) {
@@ -482,14 +587,14 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
   hipStream_t st = ctx->stream;
-  LK(launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
-  LK(launch_fav_sig(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rP, rS));
-  LK(launch_fav_hash(st, B, d_msgs, status, H));
-  LK(launch_g2_sum_jac(st, rS, B, tmp, S));
-  LK(launch_sig_pair(st, S, rP + B, H + B));
+  PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
+  PROF(1, launch_fav_sig(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rP, rS));
+  PROF(2, launch_fav_hash(st, B, d_msgs, status, H));
+  PROF(3, launch_g2_sum_jac(st, rS, B, tmp, S));
+  PROF(4, launch_sig_pair(st, S, rP + B, H + B));
   HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));
-  LK(launch_miller(st, rP, H, status, B + 1, f));
-  LK(launch_fp12_prod(st, f, B + 1, ft, fo));
+  PROF(5, launch_miller(st, rP, H, status, B + 1, f));
+  PROF(6, launch_fp12_prod(st, f, B + 1, ft, fo));
   ctx->fav_B = B;
   ctx->fav_ready = true;
   *out_f = fo;
@@ -504,10 +609,10 @@ static int fav_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   size_t B = ctx->fav_B;
   int* status = (int*)ctx->buf[S_STATUS].p;
   if (batch_ok) {
-    LK(launch_status_to_u8(ctx->stream, status, B, d_out));
+    PROF(8, launch_status_to_u8(ctx->stream, status, B, d_out));
   } else {
-    LK(launch_fav_single(ctx->stream, B, (G1A*)ctx->buf[S_APKA].p, (G2A*)ctx->buf[S_H].p, (G2A*)ctx->buf[S_SIG].p,
-                         status, d_out));
+    PROF(8, launch_fav_single(ctx->stream, B, (G1A*)ctx->buf[S_APKA].p, (G2A*)ctx->buf[S_H].p,
+                              (G2A*)ctx->buf[S_SIG].p, status, d_out));
   }
   return 0;
 }
@@ -638,7 +743,7 @@ int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
   SCR(S_FCHK, 1, out);
   CK(h2d(ctx, d_b, partials576, 576 * n));
   LK(launch_fp12_from_bytes(ctx->stream, d_b, n, fbase));
-  LK(launch_fp12_prod(ctx->stream, fbase, n, ft, out));
+  PROF(9, launch_fp12_prod(ctx->stream, fbase, n, ft, out));
   return run_final_check(ctx, out);
 }
 

@@ -185,8 +185,11 @@ BLS_HDNI Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
 // [k]p for a 256-bit scalar given as 8 little-endian u32 limbs
 template <class F>
 BLS_HDNI Jac<F> jac_mul_u256(const Jac<F>& p, const uint32_t* k) {
-  Jac<F> r = jac_identity<F>();
-  for (int i = 255; i >= 0; --i) {
+  int top = 255;
+  while (top >= 0 && !((k[top >> 5] >> (top & 31)) & 1u)) --top;
+  if (top < 0) return jac_identity<F>();
+  Jac<F> r = p;
+  for (int i = top - 1; i >= 0; --i) {
     r = jac_dbl(r);
     if ((k[i >> 5] >> (i & 31)) & 1u) r = jac_add(r, p);
   }

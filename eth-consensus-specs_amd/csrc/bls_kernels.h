@@ -29,5 +29,6 @@ hipError_t launch_verify_indexed(hipStream_t st, const uint32_t* idx, size_t B, 
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out);
 hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, Fp12* f);
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96);
+hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok, uint8_t* out48);
 
 }  // namespace bls

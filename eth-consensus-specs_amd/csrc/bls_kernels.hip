@@ -352,6 +352,40 @@ __global__ void k_fp12_from_bytes(const uint8_t* in, size_t n, Fp12* f) {
   f[i] = r;
 }
 
+// Synthetic registry: pk_i = (first + i) * G1, affine, valid.  One lane
+// walks a chunk of consecutive multiples (mixed additions of G1) and
+// normalises the chunk with one inversion (Montgomery's batch trick).
+__global__ void __launch_bounds__(64) k_registry_generate(uint64_t first, size_t n, uint32_t chunk, G1J* tmpJ,
+                                                          G1A* reg, uint8_t* reg_ok, uint8_t* out48) {
+  size_t t = gtid();
+  size_t lo = t * chunk;
+  if (lo >= n) return;
+  size_t hi = lo + chunk < n ? lo + chunk : n;
+  uint64_t k0 = first + lo;
+  uint32_t k[8] = {(uint32_t)k0, (uint32_t)(k0 >> 32), 0, 0, 0, 0, 0, 0};
+  const G1A g = g1_generator();
+  G1J p = jac_mul_u256(jac_from_aff(g), k);
+  // forward pass: store points, prefix products of Z in reg[].x (scratch)
+  Fp acc = FP_ONE;
+  for (size_t i = lo; i < hi; i++) {
+    tmpJ[i] = p;
+    acc = fp_mul(acc, p.z);
+    reg[i].y = acc;  // prefix product up to i
+    p = jac_add_aff(p, g);
+  }
+  Fp inv = fp_inv(acc);
+  for (size_t i = hi; i-- > lo;) {
+    Fp prev = (i > lo) ? reg[i - 1].y : FP_ONE;
+    Fp zi = fp_mul(inv, prev);  // 1/Z_i
+    inv = fp_mul(inv, tmpJ[i].z);
+    Fp zi2 = fp_sqr(zi);
+    G1A a{fp_mul(tmpJ[i].x, zi2), fp_mul(fp_mul(tmpJ[i].y, zi2), zi), false};
+    reg[i] = a;
+    reg_ok[i] = 1;
+    if (out48) g1_compress(out48 + 48 * i, a);
+  }
+}
+
 // ======================================================= host launchers ==
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
@@ -495,6 +529,14 @@ hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out) {
 hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, Fp12* f) {
   if (!n) return hipSuccess;
   LAUNCH(k_fp12_from_bytes, nblk(n, 64), 64, st, in, n, f);
+  return hipSuccess;
+}
+hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok,
+                                    uint8_t* out48) {
+  if (!n) return hipSuccess;
+  const uint32_t chunk = 32;
+  size_t threads = (n + chunk - 1) / chunk;
+  LAUNCH(k_registry_generate, nblk(threads, 64), 64, st, first, n, chunk, tmpJ, reg, reg_ok, out48);
   return hipSuccess;
 }
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96) {

@@ -100,6 +100,11 @@ int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* off
 int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const uint8_t* msgs32,
                              const uint8_t* sigs96, uint8_t* out);
 
+/* Synthetic registry for benchmarks: pk_i = (first_sk + i) * G1 written
+ * straight into the HBM registry (all valid); compressed keys are copied
+ * to out_pks48 when non-NULL.  Returns 1 or BLS_E_*. */
+int bls_registry_generate(bls_ctx* ctx, uint64_t first_sk, size_t n, uint8_t* out_pks48);
+
 /* Synthetic-data helpers (used by bench.py and tests to make inputs). */
 int bls_sign_batch(bls_ctx* ctx, const uint8_t* sks32, const uint8_t* msgs32, size_t B, uint8_t* out96);
 int bls_sk_to_pk_batch(bls_ctx* ctx, const uint8_t* sks32, size_t B, uint8_t* out48);
@@ -113,8 +118,8 @@ int bls_sync(bls_ctx* ctx);
 
 /* Phase 1 of a (possibly multi-GPU) FAV batch on device pointers: per-item
  * checks and this shard's Miller-loop product, written to partial576 (host,
- * 576 bytes: 12 Fp2 coefficients, big-endian).  d_status (device, B ints)
- * receives the per-item pre-pairing validity.  seed32 keys the RLC scalars. */
+ * 576 bytes: the 6 w-basis Fp2 coefficients, each c0||c1 big-endian).
+ * seed32 keys the RLC scalars.  Per-item state stays in the context. */
 int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
                               const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32,
                               uint8_t* partial576);
@@ -124,6 +129,12 @@ int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n);
  * bls_fav_batch_partial_dev call on this context.  batch_ok = result of
  * bls_partials_check; when 0 every item is re-checked individually. */
 int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out);
+
+/* ---- tracing: hipEvent time per kernel of the FAV path ------------------ */
+int bls_profile_enable(bls_ctx* ctx, int on);  /* also resets the totals */
+/* Fills up to max entries of total_ms / counts; returns the entry count. */
+int bls_profile_read(bls_ctx* ctx, double* total_ms, uint64_t* counts, int max);
+const char* bls_profile_name(int i);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace --stats database (rocpd SQLite) into a
+per-kernel table (calls, total/avg/min/max duration, VGPRs, scratch)."""
+import sqlite3
+import sys
+
+
+def main(db, out=None):
+    c = sqlite3.connect(db)
+    rows = c.execute(
+        "select name, count(*), sum(duration), avg(duration), min(duration), max(duration), "
+        "max(vgpr_count), max(accum_vgpr_count), max(scratch_size), max(grid_x), max(workgroup_x) "
+        "from kernels group by name order by sum(duration) desc").fetchall()
+    total = sum(r[2] for r in rows)
+    lines = [f"# rocprofv3 --kernel-trace --stats summary of {db}",
+             "| kernel | calls | total ms | avg ms | min ms | max ms | % | VGPR | AGPR | scratch B/lane | grid | wg |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    for name, n, tot, avg, mn, mx, vg, ag, scr, gx, wg in rows:
+        short = name.split("(")[0].replace("void ", "")
+        lines.append(f"| {short} | {n} | {tot/1e6:.3f} | {avg/1e6:.4f} | {mn/1e6:.4f} | {mx/1e6:.4f} | "
+                     f"{100*tot/total:.1f} | {vg} | {ag} | {scr} | {gx} | {wg} |")
+    text = "\n".join(lines) + "\n"
+    if out:
+        open(out, "w").write(text)
+    print(text)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
