@@ -181,7 +181,7 @@ void prof_collect(bls_ctx* c) {
 int run_final_check(bls_ctx* ctx, const Fp12* f) {
   int* d_r;
   SCR(S_INT, 4, d_r);
-  PROF(7, launch_final_check(ctx->stream, f, d_r));
+  PROF(7, launch_final_check_wave(ctx->stream, f, d_r));
   int r = 0;
   CK(d2h(ctx, &r, d_r, sizeof r));
   return r ? 1 : 0;
@@ -330,7 +330,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   LK(launch_hash_many(ctx->stream, d_msgs, d_offs, n, nullptr, 0, Q));
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->stream, P + n);
   LK(hipGetLastError());
-  LK(launch_miller(ctx->stream, P, Q, nullptr, n + 1, f));
+  LK(launch_miller_wave(ctx->stream, P, Q, nullptr, n + 1, f));
   LK(launch_fp12_prod(ctx->stream, f, n + 1, ft, fo));
   return run_final_check(ctx, fo);
 }
@@ -593,7 +593,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   PROF(3, launch_g2_sum_jac(st, rS, B, tmp, S));
   PROF(4, launch_sig_pair(st, S, rP + B, H + B));
   HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));
-  PROF(5, launch_miller(st, rP, H, status, B + 1, f));
+  PROF(5, launch_miller_wave(st, rP, H, status, B + 1, f));
   PROF(6, launch_fp12_prod(st, f, B + 1, ft, fo));
   ctx->fav_B = B;
   ctx->fav_ready = true;

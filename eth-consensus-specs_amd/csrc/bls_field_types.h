@@ -1,8 +1,8 @@
 // Field / point storage types for the MI355X BLS12-381 backend.
 //
-// Fp is one 381-bit residue in Montgomery form (R = 2^384) held as 12 x 32-bit
-// little-endian limbs: exactly the operand width of v_mad_u64_u32, so one limb
-// product is one instruction.  Every arithmetic routine is __host__ __device__
+// Fp is one 381-bit residue in Montgomery form (R = 2^406) stored as 12 x
+// 32-bit little-endian limbs (48 B, 16-B aligned for b128 LDS/global access);
+// multiplication unpacks it to 14 radix-2^29 digits (bls_fp.h).  Every arithmetic routine is __host__ __device__
 // so the same source is unit-tested on the host (tests/hostcheck) and run in
 // the gfx950 kernels.
 #pragma once
@@ -14,7 +14,7 @@
 
 namespace bls {
 
-struct Fp {
+struct alignas(16) Fp {
   uint32_t l[12];
 };
 struct Fp2 {

@@ -1,8 +1,6 @@
-// 381-bit prime-field arithmetic (Montgomery, R = 2^384, 12 x u32 limbs).
-//
-// Multiplication is CIOS: each limb product a_j * b_i + t_j + carry is one
-// 64-bit multiply-add, which hipcc lowers to v_mad_u64_u32 on gfx950
-// (288 per multiplication = one "FME" of the roofline model).
+// 381-bit prime-field arithmetic: Montgomery form with R = 2^406, stored as
+// 12 x u32 limbs, multiplied as 14 radix-2^29 digits (see fp_mul).  One
+// multiplication is the "FME" unit of the roofline model.
 // All results are fully reduced to [0, p).
 #pragma once
 #include "bls_constants.h"
@@ -38,28 +36,21 @@ BLS_HD Fp fp_select(bool c, const Fp& a, const Fp& b) {
   return r;
 }
 
-// s - p if s >= p else s   (s < 2p)
+// s - p if s >= p else s   (s < 2p).  __builtin_addc/subc lower to
+// v_add_co/v_addc_co (v_sub_co/v_subb_co) carry chains on gfx950.
 BLS_HD Fp fp_reduce_once(const Fp& s) {
   Fp d;
-  uint32_t br = 0;
+  unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)s.l[i] - P_LIMBS[i] - br;
-    d.l[i] = (uint32_t)t;
-    br = (uint32_t)(t >> 63);
-  }
+  for (int i = 0; i < 12; i++) d.l[i] = __builtin_subc(s.l[i], P_LIMBS[i], br, &br);
   return fp_select(br != 0, s, d);
 }
 
 BLS_HD Fp fp_add(const Fp& a, const Fp& b) {
   Fp s;
-  uint32_t c = 0;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)a.l[i] + b.l[i] + c;
-    s.l[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
+  for (int i = 0; i < 12; i++) s.l[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
   return fp_reduce_once(s);  // a + b < 2p < 2^382: no carry out of limb 11
 }
 
@@ -67,23 +58,15 @@ BLS_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 
 BLS_HD Fp fp_sub(const Fp& a, const Fp& b) {
   Fp d;
-  uint32_t br = 0;
+  unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)a.l[i] - b.l[i] - br;
-    d.l[i] = (uint32_t)t;
-    br = (uint32_t)(t >> 63);
-  }
+  for (int i = 0; i < 12; i++) d.l[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
   // add p back if we borrowed
-  Fp e;
-  uint32_t c = 0;
   const uint32_t m = br ? 0xffffffffu : 0u;
+  Fp e;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)d.l[i] + (P_LIMBS[i] & m) + c;
-    e.l[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
+  for (int i = 0; i < 12; i++) e.l[i] = __builtin_addc(d.l[i], P_LIMBS[i] & m, c, &c);
   return e;
 }
 
@@ -95,44 +78,99 @@ BLS_HD Fp fp_neg(const Fp& a) {
   return fp_select(fp_is_zero(a), a, d);
 }
 
-// Montgomery product a*b/R mod p; valid for a < R, b < p (result < p).
-BLS_HDNI Fp fp_mul(const Fp& a, const Fp& b) {
-  uint32_t t[13];
+// ---- Montgomery multiplication ------------------------------------------
+// Operands are stored packed (12 x u32) but multiplied as 14 digits of
+// radix 2^29 with R = 2^(14*29) = 2^406, product-scanning (FIPS) order: a
+// column of up to 28 digit products (< 2^58 each) plus the incoming carry
+// fits one 64-bit accumulator, so every digit product is exactly one
+// v_mad_u64_u32 with the running accumulator as its 64-bit addend -- no
+// carry propagation or register moves inside a column.  ~390 mads + ~160
+// other VALU ops per product (the 32-bit CIOS form compiled to ~1,280).
+BLS_HD void fp_unpack29(uint32_t d[14], const Fp& a) {
 #pragma unroll
-  for (int j = 0; j < 13; j++) t[j] = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 12; j++) {
-      uint64_t x = (uint64_t)a.l[j] * b.l[i] + t[j] + c;
-      t[j] = (uint32_t)x;
-      c = x >> 32;
-    }
-    uint64_t s = (uint64_t)t[12] + c;
-    uint32_t top = (uint32_t)(s >> 32);
-    t[12] = (uint32_t)s;
-    const uint32_t m = t[0] * P_NINV;
-    uint64_t x = (uint64_t)m * P_LIMBS[0] + t[0];
-    c = x >> 32;
-#pragma unroll
-    for (int j = 1; j < 12; j++) {
-      x = (uint64_t)m * P_LIMBS[j] + t[j] + c;
-      t[j - 1] = (uint32_t)x;
-      c = x >> 32;
-    }
-    s = (uint64_t)t[12] + c;
-    t[11] = (uint32_t)s;
-    t[12] = top + (uint32_t)(s >> 32);
+  for (int k = 0; k < 14; k++) {
+    const int bit = 29 * k, w = bit >> 5, sh = bit & 31;
+    uint32_t v = a.l[w] >> sh;
+    if (sh > 3 && w + 1 < 12) v |= a.l[w + 1] << (32 - sh);
+    d[k] = v & 0x1fffffffu;
   }
-  Fp r;
-#pragma unroll
-  for (int j = 0; j < 12; j++) r.l[j] = t[j];
-  // t < 2p and t[12] == 0 because p < R/4
-  return fp_reduce_once(r);
 }
 
-BLS_HDNI Fp fp_sqr(const Fp& a) { return fp_mul(a, a); }
+BLS_HD Fp fp_pack29(const uint32_t r[14]) {
+  Fp o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o.l[i] = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const int bit = 29 * k, w = bit >> 5, sh = bit & 31;
+    if (w < 12) o.l[w] |= r[k] << sh;
+    if (sh > 3 && w + 1 < 12) o.l[w + 1] |= r[k] >> (32 - sh);
+  }
+  return o;
+}
+
+// Montgomery product a*b/R mod p (R = 2^406); valid for a < 2^406, b < p.
+BLS_HDNI Fp fp_mul(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14], m[14], r[14];
+  fp_unpack29(x, a);
+  fp_unpack29(y, b);
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 14) acc += (uint64_t)x[i] * y[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 1 && j < 14 && i < k) acc += (uint64_t)m[i] * P29[j];
+    }
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * P29_NINV) & 0x1fffffffu;
+      acc += (uint64_t)m[k] * P29[0];
+    } else {
+      r[k - 14] = (uint32_t)acc & 0x1fffffffu;
+    }
+    acc >>= 29;
+  }
+  r[13] = (uint32_t)acc;  // result < 2p < 2^382
+  return fp_reduce_once(fp_pack29(r));
+}
+
+// Squaring: off-diagonal digit products once, doubled (105 + 14 instead of
+// 196 products for the a*a half).
+BLS_HDNI Fp fp_sqr(const Fp& a) {
+  uint32_t x[14], m[14], r[14];
+  fp_unpack29(x, a);
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    uint64_t od = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j > i && j < 14) od += (uint64_t)x[i] * x[j];
+    }
+    acc += od << 1;
+    if ((k & 1) == 0 && (k >> 1) < 14) acc += (uint64_t)x[k >> 1] * x[k >> 1];
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 1 && j < 14 && i < k) acc += (uint64_t)m[i] * P29[j];
+    }
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * P29_NINV) & 0x1fffffffu;
+      acc += (uint64_t)m[k] * P29[0];
+    } else {
+      r[k - 14] = (uint32_t)acc & 0x1fffffffu;
+    }
+    acc >>= 29;
+  }
+  r[13] = (uint32_t)acc;
+  return fp_reduce_once(fp_pack29(r));
+}
 
 // a^e for a fixed exponent given as 12 limbs with known bit length.
 BLS_HDNI Fp fp_pow(const Fp& a, const uint32_t* e, int nbits) {
@@ -144,7 +182,85 @@ BLS_HDNI Fp fp_pow(const Fp& a, const uint32_t* e, int nbits) {
   return r;
 }
 
-BLS_HDNI Fp fp_inv(const Fp& a) { return fp_pow(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
+// raw compare: a < b
+BLS_HD bool raw_lt(const uint32_t* a, const uint32_t* b) {
+  for (int i = 11; i >= 0; --i) {
+    if (a[i] != b[i]) return a[i] < b[i];
+  }
+  return false;
+}
+
+// ---- binary extended Euclid (variable time; inputs are public data) ----
+BLS_HD bool raw_is_even(const Fp& a) { return (a.l[0] & 1u) == 0; }
+BLS_HD bool raw_is_one(const Fp& a) {
+  uint32_t o = a.l[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 12; i++) o |= a.l[i];
+  return o == 0;
+}
+BLS_HD void raw_shr1(Fp& a, uint32_t top) {
+#pragma unroll
+  for (int i = 0; i < 11; i++) a.l[i] = (a.l[i] >> 1) | (a.l[i + 1] << 31);
+  a.l[11] = (a.l[11] >> 1) | (top << 31);
+}
+// a = a - b (raw, a >= b)
+BLS_HD void raw_sub(Fp& a, const Fp& b) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)a.l[i] - b.l[i] - br;
+    a.l[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+}
+BLS_HD bool raw_geq(const Fp& a, const Fp& b) { return !raw_lt(a.l, b.l); }
+// x / 2 mod p for x < p
+BLS_HD void half_mod_p(Fp& x) {
+  if (raw_is_even(x)) {
+    raw_shr1(x, 0);
+    return;
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)x.l[i] + P_LIMBS[i] + c;
+    x.l[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  raw_shr1(x, c);
+}
+
+// Inverse in Montgomery form: (aR)^-1 by binary extended Euclid on the raw
+// residue, then * R^3 / R.  ~2*381 shift/subtract steps instead of the 570
+// Montgomery multiplications of Fermat.  0 maps to 0.
+BLS_HDNI Fp fp_inv(const Fp& a) {
+  if (fp_is_zero(a)) return a;
+  Fp u = a, v, x1 = fp_zero(), x2 = fp_zero();
+#pragma unroll
+  for (int i = 0; i < 12; i++) v.l[i] = P_LIMBS[i];
+  x1.l[0] = 1;
+  while (!raw_is_one(u) && !raw_is_one(v)) {
+    while (raw_is_even(u)) {
+      raw_shr1(u, 0);
+      half_mod_p(x1);
+    }
+    while (raw_is_even(v)) {
+      raw_shr1(v, 0);
+      half_mod_p(x2);
+    }
+    if (raw_geq(u, v)) {
+      raw_sub(u, v);
+      x1 = fp_sub(x1, x2);
+    } else {
+      raw_sub(v, u);
+      x2 = fp_sub(x2, x1);
+    }
+  }
+  Fp r = raw_is_one(u) ? x1 : x2;
+  return fp_mul(r, FP_R3);
+}
+
+BLS_HDNI Fp fp_inv_fermat(const Fp& a) { return fp_pow(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
 
 BLS_HD bool fp_is_one(const Fp& a) { return fp_eq(a, FP_ONE); }
 
@@ -175,13 +291,6 @@ BLS_HD Fp fp_from_mont(const Fp& a) {
   return fp_mul(a, one);
 }
 
-// raw compare: a < b
-BLS_HD bool raw_lt(const uint32_t* a, const uint32_t* b) {
-  for (int i = 11; i >= 0; --i) {
-    if (a[i] != b[i]) return a[i] < b[i];
-  }
-  return false;
-}
 
 // canonical (non-Montgomery) integer limbs > (p-1)/2
 BLS_HD bool raw_gt_half(const Fp& canon) { return raw_lt(P_HALF, canon.l); }

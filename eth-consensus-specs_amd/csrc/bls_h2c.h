@@ -9,7 +9,7 @@
 
 namespace bls {
 
-// 64 big-endian bytes mod p -> Montgomery form: lo*R^2/R + hi*R^3/R
+// 64 big-endian bytes mod p -> Montgomery form: lo*R^2/R + hi*(2^384 R^2)/R
 BLS_HDNI Fp fp_from_be64_mod(const uint8_t* b) {
   Fp lo = raw_from_be48(b + 16);
   Fp hi = fp_zero();
@@ -17,7 +17,7 @@ BLS_HDNI Fp fp_from_be64_mod(const uint8_t* b) {
     const uint8_t* q = b + 12 - 4 * i;
     hi.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
   }
-  return fp_add(fp_mul(lo, FP_R2), fp_mul(hi, FP_R3));
+  return fp_add(fp_mul(lo, FP_R2), fp_mul(hi, FP_2P384_R2));
 }
 
 BLS_HDNI void hash_to_field_fp2(Fp2 u[2], const uint8_t* msg, uint32_t msg_len, const uint8_t* dst, uint32_t dst_len) {
