@@ -32,6 +32,8 @@ struct Buf {
 struct bls_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // concurrent branch of the FAV batch (hash_to_G2)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
   std::string err;
   Buf buf[NSLOT];
@@ -140,8 +142,9 @@ int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** o
 struct ProfScope {
   bls_ctx* c;
   int id;
+  hipStream_t st;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  ProfScope(bls_ctx* c_, int id_) : c(c_), id(id_) {
+  ProfScope(bls_ctx* c_, int id_, hipStream_t st_ = nullptr) : c(c_), id(id_), st(st_ ? st_ : c_->stream) {
     if (!c->prof_on) return;
     if (c->prof_pool.empty()) {
       hipEvent_t a, b;
@@ -150,11 +153,11 @@ struct ProfScope {
     }
     ev = c->prof_pool.back();
     c->prof_pool.pop_back();
-    (void)hipEventRecord(ev.first, c->stream);
+    (void)hipEventRecord(ev.first, st);
   }
   ~ProfScope() {
     if (!ev.first) return;
-    (void)hipEventRecord(ev.second, c->stream);
+    (void)hipEventRecord(ev.second, st);
     c->prof_pending.push_back({id, ev});
   }
 };
@@ -175,6 +178,11 @@ void prof_collect(bls_ctx* c) {
 #define PROF(id, expr)          \
   do {                          \
     ProfScope ps_(ctx, id);     \
+    LK(expr);                   \
+  } while (0)
+#define PROF2(id, st, expr)     \
+  do {                          \
+    ProfScope ps_(ctx, id, st); \
     LK(expr);                   \
   } while (0)
 
@@ -212,7 +220,10 @@ int bls_ctx_create(int device, bls_ctx** out) {
   bls_ctx* c = new (std::nothrow) bls_ctx();
   if (!c) return BLS_E_DEVICE;
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return BLS_E_DEVICE;
   }
@@ -233,6 +244,10 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   }
   if (ctx->reg) (void)hipFree(ctx->reg);
   if (ctx->reg_ok) (void)hipFree(ctx->reg_ok);
+  (void)hipStreamSynchronize(ctx->stream2);
+  (void)hipEventDestroy(ctx->ev_fork);
+  (void)hipEventDestroy(ctx->ev_join);
+  (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -587,12 +602,18 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
   hipStream_t st = ctx->stream;
+  // fork: hash_to_G2 of every message runs on stream2 beside the gather /
+  // signature branch; both join before the Miller loops.
+  HIPCK(hipEventRecord(ctx->ev_fork, st));
+  HIPCK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+  PROF2(2, ctx->stream2, launch_fav_hash(ctx->stream2, B, d_msgs, nullptr, H));
+  HIPCK(hipEventRecord(ctx->ev_join, ctx->stream2));
   PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
   PROF(1, launch_fav_sig(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rP, rS));
-  PROF(2, launch_fav_hash(st, B, d_msgs, status, H));
   PROF(3, launch_g2_sum_jac(st, rS, B, tmp, S));
   PROF(4, launch_sig_pair(st, S, rP + B, H + B));
   HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));
+  HIPCK(hipStreamWaitEvent(st, ctx->ev_join, 0));
   PROF(5, launch_miller_wave(st, rP, H, status, B + 1, f));
   PROF(6, launch_fp12_prod(st, f, B + 1, ft, fo));
   ctx->fav_B = B;

@@ -109,11 +109,23 @@ BLS_HD Fp fp_pack29(const uint32_t r[14]) {
   return o;
 }
 
-// Montgomery product a*b/R mod p (R = 2^406); valid for a < 2^406, b < p.
-BLS_HDNI Fp fp_mul(const Fp& a, const Fp& b) {
-  uint32_t x[14], y[14], m[14], r[14];
-  fp_unpack29(x, a);
-  fp_unpack29(y, b);
+// 13-limb (416-bit) value -> 14 radix-2^29 digits (top digit keeps bits 377..405)
+BLS_HD void fp_unpack29_wide(uint32_t d[14], const uint32_t* a) {
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const int bit = 29 * k, w = bit >> 5, sh = bit & 31;
+    uint32_t v = a[w] >> sh;
+    if (sh > 3 && w + 1 < 13) v |= a[w + 1] << (32 - sh);
+    d[k] = k == 13 ? (v & 0x1fffffffu) : (v & 0x1fffffffu);
+  }
+}
+
+// Montgomery product of digit vectors; with x*y < p * 2^406 the result is < 2p
+// and one conditional subtraction makes it canonical.  Any operands below
+// 2^390 qualify (x*y/R < 2^374 < p), which lets wave programs feed unreduced
+// linear combinations straight in (bls_wave.h).
+BLS_HD Fp fp_mul_digits(const uint32_t x[14], const uint32_t y[14]) {
+  uint32_t m[14], r[14];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 27; k++) {
@@ -137,6 +149,14 @@ BLS_HDNI Fp fp_mul(const Fp& a, const Fp& b) {
   }
   r[13] = (uint32_t)acc;  // result < 2p < 2^382
   return fp_reduce_once(fp_pack29(r));
+}
+
+// Montgomery product a*b/R mod p (R = 2^406); valid for a < 2^406, b < p.
+BLS_HDNI Fp fp_mul(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14];
+  fp_unpack29(x, a);
+  fp_unpack29(y, b);
+  return fp_mul_digits(x, y);
 }
 
 // Squaring: off-diagonal digit products once, doubled (105 + 14 instead of
@@ -270,10 +290,7 @@ BLS_HDNI bool fp_sqrt(Fp& out, const Fp& a) {
   return fp_eq(fp_sqr(out), a);
 }
 
-BLS_HDNI bool fp_is_square(const Fp& a) {
-  if (fp_is_zero(a)) return true;
-  return fp_is_one(fp_pow(a, EXP_LEGENDRE, EXP_LEGENDRE_BITS));
-}
+
 
 BLS_HD Fp fp_mul_small(const Fp& a, int k) {  // small positive k
   Fp r = a;
@@ -317,6 +334,38 @@ BLS_HD void raw_to_be48(const Fp& r, uint8_t* b) {
     q[2] = (uint8_t)(r.l[i] >> 8);
     q[3] = (uint8_t)r.l[i];
   }
+}
+
+// Quadratic residuosity by the binary Jacobi-symbol algorithm (variable
+// time, public inputs), ~2*381 shift/subtract steps instead of a 380-bit
+// exponentiation.  Montgomery form does not change the answer:
+// (aR/p) = (a/p)(2/p)^406 = (a/p).
+BLS_HDNI bool fp_is_square(const Fp& a_mont) {
+  if (fp_is_zero(a_mont)) return true;
+  Fp a = a_mont, n;
+#pragma unroll
+  for (int i = 0; i < 12; i++) n.l[i] = P_LIMBS[i];
+  int t = 1;
+  while (!fp_is_zero(a)) {
+    while (raw_is_even(a)) {
+      raw_shr1(a, 0);
+      const uint32_t r = n.l[0] & 7u;
+      if (r == 3u || r == 5u) t = -t;
+    }
+    if (raw_lt(a.l, n.l)) {
+      Fp tmp = a;
+      a = n;
+      n = tmp;
+      if ((a.l[0] & 3u) == 3u && (n.l[0] & 3u) == 3u) t = -t;
+    }
+    raw_sub(a, n);
+  }
+  return raw_is_one(n) && t == 1;
+}
+
+BLS_HDNI bool fp_is_square_euler(const Fp& a) {
+  if (fp_is_zero(a)) return true;
+  return fp_is_one(fp_pow(a, EXP_LEGENDRE, EXP_LEGENDRE_BITS));
 }
 
 }  // namespace bls

@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(64) k_fav_sig(size_t B, const uint8_t* msgs32,
 __global__ void __launch_bounds__(64) k_fav_hash(size_t B, const uint8_t* msgs32, const int* status, G2A* H) {
   size_t i = gtid();
   if (i >= B) return;
-  if (!status[i]) {
+  if (status && !status[i]) {
     H[i] = G2A{fp2_zero(), fp2_zero(), true};
     return;
   }

@@ -52,10 +52,13 @@ BLS_HD Fp2 fp2_mul_small(const Fp2& a, int k) { return Fp2{fp_mul_small(a.c0, k)
 BLS_HDNI bool fp2_is_square(const Fp2& a) { return fp_is_square(fp2_norm(a)); }
 
 // Some square root of a (norm method); returns false if none exists.
+// Cost: two Fp square-root exponentiations, one Jacobi symbol, one binary
+// inversion (the Jacobi symbol picks the right half-norm candidate first).
 BLS_HDNI bool fp2_sqrt(Fp2& out, const Fp2& a) {
   if (fp_is_zero(a.c1)) {
     Fp s;
-    if (fp_sqrt(s, a.c0)) {
+    if (fp_is_square(a.c0)) {
+      fp_sqrt(s, a.c0);
       out = Fp2{s, fp_zero()};
       return true;
     }
@@ -68,11 +71,9 @@ BLS_HDNI bool fp2_sqrt(Fp2& out, const Fp2& a) {
   Fp n;
   if (!fp_sqrt(n, fp2_norm(a))) return false;
   Fp t = fp_mul(fp_add(a.c0, n), FP_INV2);
+  if (!fp_is_square(t)) t = fp_mul(fp_sub(a.c0, n), FP_INV2);
   Fp x0;
-  if (!fp_sqrt(x0, t)) {
-    t = fp_mul(fp_sub(a.c0, n), FP_INV2);
-    if (!fp_sqrt(x0, t)) return false;
-  }
+  if (!fp_sqrt(x0, t)) return false;
   Fp x1 = fp_mul(a.c1, fp_inv(fp_dbl(x0)));
   Fp2 r{x0, x1};
   out = r;

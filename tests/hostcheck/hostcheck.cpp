@@ -87,3 +87,5 @@ void hc_g1_mul_u256(const uint8_t* p, const uint32_t* k, uint8_t* o48) {
   g1_compress(o48, jac_to_aff(jac_mul_u256(j, k)));
 }
 }
+extern "C" int hc_fp_is_square(const uint8_t* a) { return fp_is_square(in_fp(a)); }
+extern "C" void hc_fp_sqr(const uint8_t* a, uint8_t* o) { out_fp(o, fp_sqr(in_fp(a))); }

@@ -186,3 +186,12 @@ def test_core_verify_known_answer():
     assert H.call("hc_core_verify", pk, root, 32, O.DST_POP, len(O.DST_POP), sig) == 1
     bad = bytes([root[0] ^ 1]) + root[1:]
     assert H.call("hc_core_verify", pk, bad, 32, O.DST_POP, len(O.DST_POP), sig) == 0
+
+
+def test_jacobi_and_sqr():
+    for _ in range(200):
+        a = rfp()
+        assert H.call("hc_fp_is_square", H.fp_b(a)) == (1 if O.fp_is_square(a) else 0)
+        assert H.b_fp(H.call("hc_fp_sqr", H.fp_b(a), out=48)) == a * a % O.P
+    for a in (0, 1, O.P - 1, 4, 2):
+        assert H.call("hc_fp_is_square", H.fp_b(a)) == (1 if O.fp_is_square(a) else 0)
