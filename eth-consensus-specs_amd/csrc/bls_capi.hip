@@ -186,10 +186,10 @@ void prof_collect(bls_ctx* c) {
     LK(expr);                   \
   } while (0)
 
-int run_final_check(bls_ctx* ctx, const Fp12* f) {
+int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
   int* d_r;
   SCR(S_INT, 4, d_r);
-  PROF(7, launch_final_check_wave(ctx->stream, f, d_r));
+  PROF(7, launch_final_check_wave(ctx->stream, f, n, d_r));
   int r = 0;
   CK(d2h(ctx, &r, d_r, sizeof r));
   return r ? 1 : 0;
@@ -333,7 +333,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   SCR(S_G2A, n + 1, Q);
   SCR(S_INT, 4, d_sok);
   SCR(S_F, n + 1, f);
-  SCR(S_F_T, 512, ft);
+  SCR(S_F_T, (n + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   CK(h2d(ctx, d_sig, sig96, 96));
   LK(launch_sig_validate(ctx->stream, d_sig, 1, Q + n, d_sok));
@@ -346,7 +346,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->stream, P + n);
   LK(hipGetLastError());
   LK(launch_miller_wave(ctx->stream, P, Q, nullptr, n + 1, f));
-  LK(launch_fp12_prod(ctx->stream, f, n + 1, ft, fo));
+  LK(launch_fp12_prod_vm(ctx->stream, f, n + 1, ft, fo));
   return run_final_check(ctx, fo);
 }
 
@@ -597,7 +597,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_G2J_T, 1024, tmp);
   SCR(S_G2J, 1, S);
   SCR(S_F, B + 1, f);
-  SCR(S_F_T, 512, ft);
+  SCR(S_F_T, (B + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
@@ -615,7 +615,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));
   HIPCK(hipStreamWaitEvent(st, ctx->ev_join, 0));
   PROF(5, launch_miller_wave(st, rP, H, status, B + 1, f));
-  PROF(6, launch_fp12_prod(st, f, B + 1, ft, fo));
+  PROF(6, launch_fp12_prod_vm(st, f, B + 1, ft, fo));
   ctx->fav_B = B;
   ctx->fav_ready = true;
   *out_f = fo;
@@ -755,17 +755,12 @@ int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
   API_ENTER(ctx);
   if (!partials576 || !n) return BLS_E_ARG;
   uint8_t* d_b;
-  Fp12 *f, *ft;
+  Fp12* f;
   SCR(S_IN0, 576 * n, d_b);
-  SCR(S_F_T, 512 + n, f);
-  Fp12* fbase = f;
-  ft = fbase + n;
-  Fp12* out;
-  SCR(S_FCHK, 1, out);
+  SCR(S_FCHK, n, f);
   CK(h2d(ctx, d_b, partials576, 576 * n));
-  LK(launch_fp12_from_bytes(ctx->stream, d_b, n, fbase));
-  PROF(9, launch_fp12_prod(ctx->stream, fbase, n, ft, out));
-  return run_final_check(ctx, out);
+  PROF(9, launch_fp12_from_bytes(ctx->stream, d_b, n, f));
+  return run_final_check(ctx, f, (int)n);  // the n partials are multiplied inside the FE kernel
 }
 
 int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {

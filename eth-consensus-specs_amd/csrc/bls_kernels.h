@@ -31,6 +31,7 @@ hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, F
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96);
 hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok, uint8_t* out48);
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
-hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int* out);
+hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
+hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out);
 
 }  // namespace bls

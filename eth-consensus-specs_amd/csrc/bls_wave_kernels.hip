@@ -1,7 +1,10 @@
-// Wave-cooperative kernels: Miller loop (one 64-lane workgroup per pair) and
-// final exponentiation (one workgroup), both driven by wave programs.
+// Wave-program kernels (bls_vm.h): Miller loop (G pairs per 64-lane
+// workgroup), chunked Fp12 products, and the final exponentiation of a
+// product of partials (one workgroup).
 #include "bls_kernels.h"
-#include "bls_wave.h"
+#include "bls_vm.h"
+
+#include <stdlib.h>
 
 namespace bls {
 
@@ -24,173 +27,142 @@ __device__ __forceinline__ void load_fp12(Fp* dst, const Fp12* src) {
   if (threadIdx.x < 12) dst[threadIdx.x] = fp12_slot_src(*src, threadIdx.x);
   __syncthreads();
 }
-__device__ __forceinline__ void store_fp12(Fp12* dst, const Fp* src) {
-  if (threadIdx.x < 12) fp12_slot_dst(*dst, threadIdx.x) = src[threadIdx.x];
-  __syncthreads();
-}
+
+constexpr int imax(int a, int b) { return a > b ? a : b; }
 
 // ============================================================ Miller loop ==
-constexpr int ML_F = 0, ML_T = 12, ML_P = 18, ML_Q = 20, ML_S = 24;
-constexpr int ML_SCRATCH = (WP_ML_DBL_SCRATCH > WP_ML_ADD_SCRATCH ? WP_ML_DBL_SCRATCH : WP_ML_ADD_SCRATCH) >
-                                   WP_ML_DBL_FIRST_SCRATCH
-                               ? (WP_ML_DBL_SCRATCH > WP_ML_ADD_SCRATCH ? WP_ML_DBL_SCRATCH : WP_ML_ADD_SCRATCH)
-                               : WP_ML_DBL_FIRST_SCRATCH;
+// Item region (WL_ML_*): f (12) | T (6) | P (2: -xP, yP) | Q (4) | scratch
+constexpr int ML_G = 2;  // pairs per workgroup
 
-__global__ void __launch_bounds__(64) k_miller_wave(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* fout) {
-  __shared__ Fp slots[ML_S + ML_SCRATCH];
-  const size_t i = blockIdx.x;
-  if (i >= n) return;
+template <int G>
+__global__ void __launch_bounds__(64) k_miller_vm(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* fout) {
+  __shared__ Fp slots[WP_NCONST + G * WL_ML_STRIDE];
+  __shared__ int skip[G];
   const int lane = threadIdx.x;
-  const bool skip = (ok && !ok[i]) || P[i].inf || Q[i].inf;
-  if (skip) {
-    if (lane == 0) fout[i] = fp12_one();
-    return;
-  }
-  if (lane < 12) {
-    Fp v = fp_zero();
-    if (lane < 6) {
-      const G2A& q = Q[i];
-      const Fp2& c = lane < 2 ? q.x : (lane < 4 ? q.y : q.y);
-      v = (lane & 1) ? c.c1 : c.c0;
-      if (lane == 4) v = FP_ONE;
-      if (lane == 5) v = fp_zero();
-      slots[ML_T + lane] = v;
-    } else if (lane < 8) {
-      slots[ML_P + lane - 6] = lane == 6 ? fp_neg(P[i].x) : P[i].y;
-    } else {
-      const G2A& q = Q[i];
-      const int j = lane - 8;
-      const Fp2& c = j < 2 ? q.x : q.y;
-      slots[ML_Q + j] = (j & 1) ? c.c1 : c.c0;
-    }
+  const size_t i0 = (size_t)blockIdx.x * G;
+  vm_load_consts(slots);
+  if (lane < G) {
+    const size_t i = i0 + lane;
+    skip[lane] = i >= n || (ok && !ok[i]) || P[i].inf || Q[i].inf;
   }
   __syncthreads();
-  const int fb[5] = {ML_F, ML_T, ML_P, ML_Q, ML_S};
-  wave_run(WAVE_PROG(ML_DBL_FIRST), slots, fb);
-  if ((X_ABS >> 62) & 1ull) wave_run(WAVE_PROG(ML_ADD), slots, fb);
+  const int item0 = WP_NCONST;
+  // 12 values per pair: T (x, y, 1), P (-x, y), Q (x, y)
+  for (int k = lane; k < 12 * G; k += 64) {
+    const int g = k / 12, j = k % 12;
+    const size_t i = i0 + g;
+    Fp* r = slots + item0 + g * WL_ML_STRIDE;
+    Fp v = fp_zero();
+    if (!skip[g]) {
+      const G2A& q = Q[i];
+      if (j < 4) v = (j & 1) ? (j < 2 ? q.x.c1 : q.y.c1) : (j < 2 ? q.x.c0 : q.y.c0);
+      else if (j == 4) v = FP_ONE;
+      else if (j == 6) v = fp_neg(P[i].x);
+      else if (j == 7) v = P[i].y;
+      else if (j >= 8) v = (j & 1) ? (j < 10 ? q.x.c1 : q.y.c1) : (j < 10 ? q.x.c0 : q.y.c0);
+    }
+    if (j < 6) r[WL_ML_T + j] = v;
+    else if (j < 8) r[WL_ML_P + j - 6] = v;
+    else r[WL_ML_Q + j - 8] = v;
+  }
+  __syncthreads();
+  vm_run<G>(VM_PROG(ML_DBL_FIRST), slots, item0, WL_ML_STRIDE, nullptr);
+  if ((X_ABS >> 62) & 1ull) vm_run<G>(VM_PROG(ML_ADD), slots, item0, WL_ML_STRIDE, nullptr);
   for (int b = 61; b >= 0; --b) {
-    wave_run(WAVE_PROG(ML_DBL), slots, fb);
-    if ((X_ABS >> b) & 1ull) wave_run(WAVE_PROG(ML_ADD), slots, fb);
+    vm_run<G>(VM_PROG(ML_DBL), slots, item0, WL_ML_STRIDE, nullptr);
+    if ((X_ABS >> b) & 1ull) vm_run<G>(VM_PROG(ML_ADD), slots, item0, WL_ML_STRIDE, nullptr);
   }
   // x < 0: conjugate (negate the odd w-coefficients: slots 2,3,6,7,10,11)
-  if (lane < 12) {
-    Fp v = slots[ML_F + lane];
-    if ((lane >> 1) & 1) v = fp_neg(v);
-    fp12_slot_dst(fout[i], lane) = v;
+  for (int k = lane; k < 12 * G; k += 64) {
+    const int g = k / 12, j = k % 12;
+    const size_t i = i0 + g;
+    if (i >= n) continue;
+    Fp v = slots[item0 + g * WL_ML_STRIDE + WL_ML_F + j];
+    if ((j >> 1) & 1) v = fp_neg(v);
+    if (skip[g]) v = j == 0 ? FP_ONE : fp_zero();
+    fp12_slot_dst(fout[i], j) = v;
   }
 }
 
-// ===================================================== final exponentiation ==
-constexpr int FE_R = 6;       // 12-slot registers
-constexpr int FE_SCR = WP_FP12_MUL_SCRATCH > WP_FP12_SQR_SCRATCH ? WP_FP12_MUL_SCRATCH : WP_FP12_SQR_SCRATCH;
-constexpr int FE_S = 12 * FE_R;
-
-struct FeCtx {
-  Fp* s;
-};
-
-__device__ __forceinline__ void w_mul(Fp* s, int dst, int a, int b) {
-  const int fb[4] = {12 * a, 12 * b, 12 * dst, FE_S};
-  wave_run(WAVE_PROG(FP12_MUL), s, fb);
-}
-__device__ __forceinline__ void w_sqr(Fp* s, int dst, int a) {
-  const int fb[3] = {12 * a, 12 * dst, FE_S};
-  wave_run(WAVE_PROG(FP12_SQR), s, fb);
-}
-__device__ __forceinline__ void w_copy(Fp* s, int dst, int a) {
-  if (threadIdx.x < 12) s[12 * dst + threadIdx.x] = s[12 * a + threadIdx.x];
+// ============================================ Fp12 registers of one item ==
+// Region WL_FE_*: registers R0..R6 (12 slots each) | scratch.  Every
+// operation is a program instance bound to its registers (FE_* in wavec).
+__device__ __forceinline__ Fp* fe_reg(Fp* s, int k) { return s + WP_NCONST + 12 * k; }
+__device__ __forceinline__ void fe_run(Fp* s, const VmProg p) { vm_run<1>(p, s, WP_NCONST, 0, nullptr); }
+__device__ __forceinline__ void fe_copy(Fp* s, int dst, int a) {
+  if (threadIdx.x < 12) fe_reg(s, dst)[threadIdx.x] = fe_reg(s, a)[threadIdx.x];
   __syncthreads();
 }
-__device__ __forceinline__ void w_conj(Fp* s, int dst, int a) {
+__device__ __forceinline__ void fe_conj(Fp* s, int dst, int a) {
   if (threadIdx.x < 12) {
-    Fp v = s[12 * a + threadIdx.x];
-    s[12 * dst + threadIdx.x] = ((threadIdx.x >> 1) & 1) ? fp_neg(v) : v;
+    const Fp v = fe_reg(s, a)[threadIdx.x];
+    fe_reg(s, dst)[threadIdx.x] = ((threadIdx.x >> 1) & 1) ? fp_neg(v) : v;
   }
   __syncthreads();
 }
-// frob2: coefficient k times gamma_{2,k} in Fp (dst != a not required)
-__device__ __forceinline__ void w_frob2(Fp* s, int dst, int a) {
-  Fp v;
-  const int j = threadIdx.x;
-  if (j < 12) {
-    const int k = j >> 1;
-    const Fp g = k == 0 ? FP_ONE
-                        : (k == 1 ? FROB2_1.c0 : (k == 2 ? FROB2_2.c0 : (k == 3 ? FROB2_3.c0 : (k == 4 ? FROB2_4.c0 : FROB2_5.c0))));
-    v = k == 0 ? s[12 * a + j] : fp_mul(s[12 * a + j], g);
-  }
-  __syncthreads();
-  if (j < 12) s[12 * dst + j] = v;
-  __syncthreads();
-}
-// frob1: conj(c_k) * gamma_{1,k}
-__device__ __forceinline__ void w_frob1(Fp* s, int dst, int a) {
-  Fp v;
-  const int j = threadIdx.x;
-  if (j < 12) {
-    const int k = j >> 1;
-    const Fp2 g = k == 0 ? fp2_one()
-                         : (k == 1 ? FROB1_1 : (k == 2 ? FROB1_2 : (k == 3 ? FROB1_3 : (k == 4 ? FROB1_4 : FROB1_5))));
-    const Fp ca = s[12 * a + 2 * k], cb = s[12 * a + 2 * k + 1];
-    // (ca - cb i)(ga + gb i) = ca ga + cb gb + (ca gb - cb ga) i
-    if ((j & 1) == 0)
-      v = fp_add(fp_mul(ca, g.c0), fp_mul(cb, g.c1));
-    else
-      v = fp_sub(fp_mul(ca, g.c1), fp_mul(cb, g.c0));
-  }
-  __syncthreads();
-  if (j < 12) s[12 * dst + j] = v;
-  __syncthreads();
-}
-// dst = a^x (x = -|x|, cyclotomic: inverse = conjugate); dst != a
-__device__ void w_pow_x(Fp* s, int dst, int a) {
-  w_copy(s, dst, a);
-  for (int b = 62; b >= 0; --b) {
-    w_sqr(s, dst, dst);
-    if ((X_ABS >> b) & 1ull) w_mul(s, dst, dst, a);
-  }
-  w_conj(s, dst, dst);
+// R1 = R2^x (x = -|x|; cyclotomic input, so the inverse is the conjugate)
+__device__ void fe_pow_x(Fp* s) {
+  fe_run(s, VM_PROG(FE_POWX_0));
+  fe_run(s, VM_PROG(FE_POWX_1));
+  fe_run(s, VM_PROG(FE_POWX_2));
+  fe_run(s, VM_PROG(FE_POWX_3));
+  fe_run(s, VM_PROG(FE_POWX_4));
+  fe_run(s, VM_PROG(FE_POWX_5));
+  fe_conj(s, 1, 1);
 }
 
-__global__ void __launch_bounds__(64) k_final_check_wave(const Fp12* fin, int* out) {
-  __shared__ Fp s[FE_S + FE_SCR];
+// Product of n Fp12 values, then the final exponentiation; *out = (result == 1).
+// Easy part (p^6-1)(p^2+1); hard part via (x-1)^2 (x+p) (x^2+p^2-1) + 3, which
+// returns e^3 (e == 1 <=> e^3 == 1 since gcd(3, r) = 1).
+__global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, int* out) {
+  __shared__ Fp s[WP_NCONST + WL_FE_STRIDE];
   __shared__ Fp12 inv;
   __shared__ int okc;
   const int lane = threadIdx.x;
-  // registers: 0 = f/t, 1 = tmp, 2 = a, 3 = b, 4 = c, 5 = t3
-  load_fp12(s + 0, fin);
-  if (lane == 0) inv = fp12_inv(*fin);
+  vm_load_consts(s);
+  load_fp12(fe_reg(s, 0), fin);
+  for (int i = 1; i < n; i++) {
+    load_fp12(fe_reg(s, 1), fin + i);
+    fe_run(s, VM_PROG(FE_MUL_001));
+  }
+  if (lane == 0) {
+    Fp12 f;
+    for (int j = 0; j < 12; j++) fp12_slot_dst(f, j) = fe_reg(s, 0)[j];
+    inv = fp12_inv(f);
+  }
   __syncthreads();
-  load_fp12(s + 12, &inv);
-  w_conj(s, 2, 0);
-  w_mul(s, 0, 2, 1);  // t = conj(f) * f^-1
-  w_frob2(s, 1, 0);
-  w_mul(s, 0, 1, 0);  // t = t^(p^2) * t
+  load_fp12(fe_reg(s, 1), &inv);
+  fe_conj(s, 2, 0);
+  fe_run(s, VM_PROG(FE_MUL_021));    // t = conj(f) * f^-1
+  fe_run(s, VM_PROG(FE_FROB2_10));
+  fe_run(s, VM_PROG(FE_MUL_001));    // t = t^(p^2) * t            (R0)
   // a = t^((x-1)^2)
-  w_pow_x(s, 1, 0);
-  w_conj(s, 2, 0);
-  w_mul(s, 2, 1, 2);  // a = t^(x-1)
-  w_pow_x(s, 1, 2);
-  w_conj(s, 3, 2);
-  w_mul(s, 2, 1, 3);  // a = a^(x-1)
+  fe_copy(s, 2, 0);
+  fe_pow_x(s);                       // R1 = t^x
+  fe_conj(s, 2, 0);
+  fe_run(s, VM_PROG(FE_MUL_221));    // R2 = a = t^(x-1)
+  fe_pow_x(s);                       // R1 = a^x
+  fe_conj(s, 3, 2);
+  fe_run(s, VM_PROG(FE_MUL_213));    // R2 = a^(x-1)
   // b = a^(x+p)
-  w_pow_x(s, 1, 2);
-  w_frob1(s, 3, 2);
-  w_mul(s, 3, 1, 3);
+  fe_pow_x(s);                       // R1 = a^x
+  fe_run(s, VM_PROG(FE_FROB1_32));   // R3 = a^p
+  fe_run(s, VM_PROG(FE_MUL_331));    // R3 = b
   // c = b^(x^2+p^2-1)
-  w_pow_x(s, 1, 3);
-  w_pow_x(s, 4, 1);
-  w_frob2(s, 1, 3);
-  w_mul(s, 4, 4, 1);
-  w_conj(s, 1, 3);
-  w_mul(s, 4, 4, 1);
-  // t^3
-  w_sqr(s, 5, 0);
-  w_mul(s, 5, 5, 0);
-  w_mul(s, 4, 4, 5);
+  fe_copy(s, 2, 3);
+  fe_pow_x(s);                       // R1 = b^x
+  fe_copy(s, 2, 1);
+  fe_pow_x(s);                       // R1 = b^(x^2)
+  fe_run(s, VM_PROG(FE_FROB2_43));   // R4 = b^(p^2)
+  fe_run(s, VM_PROG(FE_MUL_114));
+  fe_conj(s, 4, 3);
+  fe_run(s, VM_PROG(FE_MUL_114));    // R1 = c
+  fe_run(s, VM_PROG(FE_CUBE));       // R5 = t^3
+  fe_run(s, VM_PROG(FE_MUL_115));
   if (lane == 0) okc = 1;
   __syncthreads();
   if (lane < 12) {
-    const Fp v = s[48 + lane];
+    const Fp v = fe_reg(s, 1)[lane];
     const bool good = lane == 0 ? fp_is_one(v) : fp_is_zero(v);
     if (!good) okc = 0;
   }
@@ -198,15 +170,61 @@ __global__ void __launch_bounds__(64) k_final_check_wave(const Fp12* fin, int* o
   if (lane == 0) *out = okc;
 }
 
+// Products of consecutive chunks: out[b] = prod in[b*chunk .. min(n, (b+1)*chunk))
+__global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n, int chunk, Fp12* outp) {
+  __shared__ Fp s[WP_NCONST + WL_CH_STRIDE];
+  const size_t lo = (size_t)blockIdx.x * chunk;
+  const size_t hi = lo + chunk < n ? lo + chunk : n;
+  vm_load_consts(s);
+  const int base = WP_NCONST;
+  load_fp12(s + base, in + lo);
+  for (size_t i = lo + 1; i < hi; i++) {
+    load_fp12(s + base + 12, in + i);
+    vm_run<1>(VM_PROG(CH_MUL), s, base, 0, nullptr);
+  }
+  if (threadIdx.x < 12) fp12_slot_dst(outp[blockIdx.x], threadIdx.x) = s[base + threadIdx.x];
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_miller_wave, dim3((unsigned)n), dim3(64), 0, st, P, Q, ok, n, f);
+  static const int g = env_int("BLS_ML_G", ML_G);  // tuning knob (pairs per workgroup)
+  if (g == 1)
+    hipLaunchKernelGGL(k_miller_vm<1>, dim3((unsigned)n), dim3(64), 0, st, P, Q, ok, n, f);
+  else if (g == 4)
+    hipLaunchKernelGGL(k_miller_vm<4>, dim3((unsigned)((n + 3) / 4)), dim3(64), 0, st, P, Q, ok, n, f);
+  else
+    hipLaunchKernelGGL(k_miller_vm<2>, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, P, Q, ok, n, f);
   return hipGetLastError();
 }
 
-hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int* out) {
-  hipLaunchKernelGGL(k_final_check_wave, dim3(1), dim3(64), 0, st, f, out);
+hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out) {
+  hipLaunchKernelGGL(k_final_check_vm, dim3(1), dim3(64), 0, st, f, n, out);
   return hipGetLastError();
+}
+
+// Product of n values into out[0] via chunked passes; tmp holds >= n/8 + 16 entries.
+hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out) {
+  const Fp12* cur = in;
+  Fp12* bufs[2] = {tmp, tmp + (n + 15) / 16 + 1};
+  int w = 0;
+  while (n > 1) {
+    const int chunk = n > 64 ? 16 : (int)n;
+    const size_t blocks = (n + chunk - 1) / chunk;
+    Fp12* dst = blocks == 1 ? out : bufs[w];
+    hipLaunchKernelGGL(k_fp12_chunk_prod, dim3((unsigned)blocks), dim3(64), 0, st, cur, n, chunk, dst);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    cur = dst;
+    n = blocks;
+    w ^= 1;
+  }
+  if (cur != out) return hipMemcpyAsync(out, cur, sizeof(Fp12), hipMemcpyDeviceToDevice, st);
+  return hipSuccess;
 }
 
 }  // namespace bls

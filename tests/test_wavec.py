@@ -1,6 +1,7 @@
 """The wave programs (tools/wavec.py -> bls_waveprog.h) evaluated by a Python
-model of the device interpreter (bls_wave.h) against the oracle: CPU-side
-proof that the traced formulas and the level schedule are right."""
+model of the device interpreter (bls_vm.h) against the oracle: CPU-side
+proof that the traced formulas, the level schedule and the slot allocation
+are right."""
 import os
 import random
 import sys
@@ -13,27 +14,36 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import wavec  # noqa: E402
 
 PROGS = {p["name"]: p for p in wavec.compile_all()}
+POOL = [v for v, _ in sorted(wavec.CONST_POOL.items(), key=lambda kv: kv[1])]
 rng = random.Random(7)
-MONT = 1 << 384
-RINV = pow(MONT, -1, O.P)
 
 
-def run(prog, frames):
-    """frames: list of lists of ints (canonical values); scratch appended. Mirrors wave_run."""
+def run(prog, frames, pred=0):
+    """frames: list of lists of canonical ints (one per program frame, scratch
+    excluded).  Mirrors vm_run for one item: every op of a level reads its
+    operands before any op of the level writes."""
     fr = [list(f) for f in frames] + [[0] * prog["frames"][-1]]
-    # Montgomery domain is transparent for lincombs; model products as a*b (canonical)
-    for ix, v in prog["consts"]:
-        fr[-1][ix] = v % O.P
+
+    def get(f, i):
+        return POOL[i] if f == wavec.CONST_FRAME else fr[f][i]
+
+    def lin(ts):
+        return sum(k * get(f, i) for f, i, k in ts) % O.P
+
     for items in prog["levels"]:
-        assert len(items) <= 64
         vals = []
         for kind, (dfr, dix), a, b in items:
-            va = sum(k * fr[f][i] for f, i, k in a) % O.P
             if kind == "mul":
-                vb = sum(k * fr[f][i] for f, i, k in b) % O.P
-                va = va * vb % O.P
-            vals.append(((dfr, dix), va))
-        for (dfr, dix), v in vals:  # all reads of a level precede its writes
+                v = lin(a) * lin(b) % O.P
+            elif kind == "sel":
+                v = lin(a) if pred & 1 else lin(b)
+            elif kind == "lut":
+                (f, i, s), = a
+                v = get(f, i + pred * s)
+            else:
+                v = lin(a)
+            vals.append(((dfr, dix), v))
+        for (dfr, dix), v in vals:
             fr[dfr][dix] = v
     return fr
 
@@ -53,19 +63,77 @@ def rf12():
     return O.f12_from_coeffs([(rng.randrange(O.P), rng.randrange(O.P)) for _ in range(6)])
 
 
-def test_fp12_mul_and_sqr_programs():
+def cyclotomic(f):
+    t = O.f12_mul(O.f12_conj(f), O.f12_inv(f))
+    return O.f12_mul(O.f12_frobenius(O.f12_frobenius(t)), t)
+
+
+def g2_proj(pt, z=None):
+    """affine oracle point -> projective Fp list with a random Z."""
+    if pt is None:
+        return [0, 0, 1, 0, 0, 0]
+    z = z or (rng.randrange(1, O.P), rng.randrange(O.P))
+    x, y = O.f2_mul(pt[0], z), O.f2_mul(pt[1], z)
+    return [x[0], x[1], y[0], y[1], z[0], z[1]]
+
+
+def g2_aff(v):
+    z = (v[4], v[5])
+    if z == (0, 0):
+        return None
+    zi = O.f2_inv(z)
+    return (O.f2_mul((v[0], v[1]), zi), O.f2_mul((v[2], v[3]), zi))
+
+
+def g1_proj(pt):
+    if pt is None:
+        return [0, 1, 0]
+    z = rng.randrange(1, O.P)
+    return [pt[0] * z % O.P, pt[1] * z % O.P, z]
+
+
+def g1_aff(v):
+    if v[2] == 0:
+        return None
+    zi = pow(v[2], -1, O.P)
+    return (v[0] * zi % O.P, v[1] * zi % O.P)
+
+
+def rand_e2_point():
+    """A point of E2 outside G2 (the image of SSWU + isogeny)."""
+    u = (rng.randrange(O.P), rng.randrange(O.P))
+    return O.iso_map(O.map_to_curve_sswu(u))
+
+
+def test_fp12_mul_sqr_frob_programs():
     for _ in range(3):
         a, b = rf12(), rf12()
         fr = run(PROGS["FP12_MUL"], [f12_list(a), f12_list(b), [0] * 12])
         assert list_f12(fr[2]) == O.f12_mul(a, b)
         fr = run(PROGS["FP12_SQR"], [f12_list(a), [0] * 12])
         assert list_f12(fr[1]) == O.f12_sqr(a)
+        fr = run(PROGS["FP12_FROB1"], [f12_list(a), [0] * 12])
+        assert list_f12(fr[1]) == O.f12_frobenius(a)
+        fr = run(PROGS["FP12_FROB2"], [f12_list(a), [0] * 12])
+        assert list_f12(fr[1]) == O.f12_frobenius(O.f12_frobenius(a))
 
 
-def test_level_widths_fit_a_wave():
+def test_cyclotomic_runs_compose_pow_x():
+    a = cyclotomic(rf12())
+    base = f12_list(a)
+    cur = base
+    for k, add in wavec.X_RUNS:
+        name = f"CYC_{k}{'M' if add else ''}"
+        cur = run(PROGS[name], [cur, base, [0] * 12])[2]
+    assert list_f12(cur) == O.f12_pow(a, O.X_ABS)
+
+
+def test_level_descriptors_are_sane():
     for p in PROGS.values():
         for items in p["levels"]:
-            assert 1 <= len(items) <= 64
+            assert len(items) >= 1
+            for kind, dst, a, b in items:
+                assert len(a) <= wavec.MAX_TERMS and len(b) <= wavec.MAX_TERMS
 
 
 @pytest.mark.parametrize("k1,k2", [(3, 5), (0x1234567, 0x7654321)])
@@ -86,3 +154,97 @@ def test_miller_loop_program_sequence(k1, k2):
             fr = run(PROGS["ML_ADD"], fr)[:4]
     ml = O.f12_conj(list_f12(fr[0]))
     assert O.final_exponentiation(ml) == O.pairing(P1, Q2)
+
+
+def test_complete_g2_arithmetic():
+    p, q = rand_e2_point(), rand_e2_point()
+    fr = run(PROGS["G2_ADD"], [g2_proj(p), g2_proj(q), [0] * 6])
+    assert g2_aff(fr[2]) == O.g2_add(p, q)
+    # exceptional inputs handled without branches: P + P, P + (-P), O + P
+    fr = run(PROGS["G2_ADD"], [g2_proj(p), g2_proj(p), [0] * 6])
+    assert g2_aff(fr[2]) == O.g2_add(p, p)
+    fr = run(PROGS["G2_ADD"], [g2_proj(p), g2_proj(O.g2_neg(p)), [0] * 6])
+    assert g2_aff(fr[2]) is None
+    fr = run(PROGS["G2_ADD"], [g2_proj(None), g2_proj(q), [0] * 6])
+    assert g2_aff(fr[2]) == q
+
+
+def test_g2_xmul_runs_compose_xabs():
+    p = rand_e2_point()
+    base = g2_proj(p)
+    cur = base
+    for k, add in wavec.X_RUNS:
+        cur = run(PROGS[f"G2X_{k}{'A' if add else ''}"], [cur, base, [0] * 6])[2]
+    assert g2_aff(cur) == O.g2_mul(p, O.X_ABS)
+
+
+@pytest.mark.parametrize("ext", [False, True])
+def test_double_and_always_add_select(ext):
+    k = rng.getrandbits(64) | 1
+    if ext:
+        p = O.g2_mul(O.G2_GEN, rng.randrange(1, O.R))
+        R = g2_proj(None)
+        q = [p[0][0], p[0][1], p[1][0], p[1][1]]
+        name, aff, mul = "G2_DAS", g2_aff, O.g2_mul
+    else:
+        p = O.g1_mul(O.G1_GEN, rng.randrange(1, O.R))
+        R = g1_proj(None)
+        q = [p[0], p[1]]
+        name, aff, mul = "G1_DAS", g1_aff, O.g1_mul
+    for b in range(63, -1, -1):
+        R = run(PROGS[name], [R, q], pred=(k >> b) & 1)[0]
+    assert aff(R) == mul(p, k)
+
+
+def test_g1_add_program():
+    a = O.g1_mul(O.G1_GEN, 11)
+    b = O.g1_mul(O.G1_GEN, 31)
+    fr = run(PROGS["G1_ADD"], [g1_proj(a), g1_proj(b), [0] * 3])
+    assert g1_aff(fr[2]) == O.g1_mul(O.G1_GEN, 42)
+
+
+def test_g2_subgroup_check_program():
+    def check(pt):
+        base = g2_proj(pt, z=(1, 0))
+        cur = base
+        for k, add in wavec.X_RUNS:
+            cur = run(PROGS[f"G2X_{k}{'A' if add else ''}"], [cur, base, [0] * 6])[2]
+        out = run(PROGS["G2_SUBCHK"], [base[:4], cur, [0] * 6])[2]
+        return out[:4] == [0, 0, 0, 0] and out[4:6] != [0, 0]
+
+    assert check(O.g2_mul(O.G2_GEN, 0x5EED))
+    assert not check(rand_e2_point())
+
+
+def test_iso_and_cofactor_programs_match_hash_to_g2():
+    msg = b"wave programs"
+    u0, u1 = O.hash_to_field_fp2(msg, 2, O.DST_POP)
+    p0, p1 = O.map_to_curve_sswu(u0), O.map_to_curve_sswu(u1)
+    frame0 = [p0[0][0], p0[0][1], p0[1][0], p0[1][1], p1[0][0], p1[0][1], p1[1][0], p1[1][1]]
+    q = run(PROGS["ISO_PAIR"], [frame0, [0] * 6])[1]
+    assert g2_aff(q) == O.g2_add(O.iso_map(p0), O.iso_map(p1))
+
+    def xmul(v):
+        cur = v
+        for k, add in wavec.X_RUNS:
+            cur = run(PROGS[f"G2X_{k}{'A' if add else ''}"], [cur, v, [0] * 6])[2]
+        return cur
+
+    m1 = xmul(q)
+    fr = run(PROGS["CLEAR_PRE"], [q, m1, [0] * 6, [0] * 6])
+    A, C = fr[2], fr[3]
+    m2 = xmul(A)
+    h = run(PROGS["CLEAR_POST"], [C, m2, [0] * 6])[2]
+    # affine via the inversion programs
+    z = (h[4], h[5])
+    n = run(PROGS["FP2_NORM"], [list(z), [0]])[1][0]
+    zi = run(PROGS["FP2_INVFIN"], [list(z), [pow(n, -1, O.P)], [0, 0]])[2]
+    xy = run(PROGS["G2_TOAFF"], [h, zi, [0] * 4])[2]
+    assert ((xy[0], xy[1]), (xy[2], xy[3])) == O.hash_to_g2(msg)
+
+
+def test_g1_to_affine_program():
+    p = O.g1_mul(O.G1_GEN, 77)
+    v = g1_proj(p)
+    xy = run(PROGS["G1_TOAFF"], [v, [pow(v[2], -1, O.P)], [0, 0]])[2]
+    assert tuple(xy) == p

@@ -1,24 +1,31 @@
 #!/usr/bin/env python3
-"""wavec -- compile extension-field formulas into wave programs (build tool).
+"""wavec -- compile extension-field / curve formulas into wave programs (build tool).
 
 A *wave program* is a straight-line program over Fp whose only non-linear
 operation is the Montgomery product.  The formulas (Fp12 multiplication,
-the Miller-loop doubling step, ...) are written once below against a
-symbolic Fp; tracing them yields a DAG of products whose operands are
-small-integer linear combinations of earlier values.  Products are then
-levelled (ASAP) so every product of a level is independent: on the device a
-64-lane wave executes one level per step, lane j computing product j
-(bls_wave.h).  The Fp12 product that costs one lane 54 sequential
-multiplications therefore costs the wave one multiplication of latency.
+cyclotomic squaring runs, Miller-loop steps, complete projective point
+arithmetic on E1 / E2, ...) are written once below against a symbolic Fp;
+tracing them yields a DAG of products whose operands are small-integer
+linear combinations of earlier values.  Products are levelled (ASAP) so
+every product of a level is independent: on the device a 64-lane workgroup
+executes one level per step for G items at once (bls_vm.h), lane work
+index k -> (op j = k / G, item g = k % G).
+
+Op kinds (2 bits in the destination word):
+  0 lin  dest = reduce(sum c_t x_t)
+  1 mul  dest = (sum a_t x_t) * (sum b_t y_t)      (Montgomery product)
+  2 sel  dest = pred[g] & 1 ? reduce(A) : reduce(B)
+  3 lut  dest = slot[frame][ix + pred[g] * stride]  (per-item table lookup)
+
+Frames: frame k < 15 of a program is a contiguous run of per-item Fp slots
+whose base the kernel passes at run time; the program's last frame is its
+private scratch.  Frame 15 is the global constant pool (WP_CONST_POOL),
+shared by all items and loaded into LDS once per workgroup.
 
 Output: eth-consensus-specs_amd/csrc/bls_waveprog.h (constant tables).
-Each program addresses slots through *frames*: frame k of a program is a
-contiguous run of Fp slots whose base the kernel passes at run time; the
-last frame is the program's private scratch (one slot per product plus the
-output temporaries).
-
 This module is standalone (no oracle import); tests/test_wavec.py checks the
-traced formulas numerically against the oracle.
+traced formulas numerically against the oracle with a Python model of the
+device interpreter.
 """
 from __future__ import annotations
 
@@ -26,15 +33,18 @@ import os
 from collections import defaultdict
 
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+X_ABS = 0xD201000000010000
+CONST_FRAME = 15
+KIND = {"lin": 0, "mul": 1, "sel": 2, "lut": 3}
 
 # --------------------------------------------------------------------------
-# symbolic Fp: a linear form over "atoms" (inputs or products)
+# symbolic Fp: a linear form over "atoms"
 # --------------------------------------------------------------------------
 
 
 class Ctx:
     def __init__(self):
-        self.atoms = []  # ('in', frame, idx) | ('prod', a_form, b_form) | ('const', value)
+        self.atoms = []  # ('in', fr, ix) | ('const', v) | ('prod', fa, fb) | ('lin', f) | ('sel', fa, fb) | ('lut', fr, ix, stride)
         self.consts = {}
 
     def atom(self, desc):
@@ -70,6 +80,8 @@ class V:
     def __mul__(self, o):
         if isinstance(o, int):
             return self.smul(o)
+        if not self.f or not o.f:
+            return V(self.c, {})
         a = self.c.atom(("prod", dict(self.f), dict(o.f)))
         return V(self.c, {a: 1})
 
@@ -85,6 +97,8 @@ def inp(c, frame, idx):
 
 def const(c, value):
     value %= P
+    if value == 0:
+        return V(c, {})
     if value not in c.consts:
         c.consts[value] = c.atom(("const", value))
     return V(c, {c.consts[value]: 1})
@@ -92,6 +106,28 @@ def const(c, value):
 
 def zero(c):
     return V(c, {})
+
+
+def mat(v: V) -> V:
+    """Materialise a linear form as a reduced slot value (a 'lin' op)."""
+    if len(v.f) == 1 and list(v.f.values())[0] == 1:
+        return v
+    return V(v.c, {v.c.atom(("lin", dict(v.f))): 1})
+
+
+def mat12(a):
+    co = [mat(x) for x in a.coeffs()]
+    w = [F2(co[2 * k], co[2 * k + 1]) for k in range(6)]
+    return F12(F6(w[0], w[2], w[4]), F6(w[1], w[3], w[5]))
+
+
+def sel(c, a: V, b: V) -> V:
+    """pred ? a : b  (per item)."""
+    return V(c, {c.atom(("sel", dict(a.f), dict(b.f))): 1})
+
+
+def lut(c, frame, idx, stride) -> V:
+    return V(c, {c.atom(("lut", frame, idx, stride)): 1})
 
 
 # --------------------------------------------------------------------------
@@ -116,10 +152,18 @@ class F2:
         return F2(s.a.smul(k), s.b.smul(k))
 
     def __mul__(s, o):
+        if isinstance(o, int):
+            return s.smul(o)
         if isinstance(o, V):  # Fp2 x Fp
             return F2(s.a * o, s.b * o)
         if s.b.is_zero() and o.b.is_zero():
             return F2(s.a * o.a, s.b)
+        if o.b.is_zero():
+            return F2(s.a * o.a, s.b * o.a)
+        if s.b.is_zero():
+            return F2(o.a * s.a, o.b * s.a)
+        if o.a.is_zero():  # (a + b i)(d i) = -b d + a d i
+            return F2(-(s.b * o.b), s.a * o.b)
         t0 = s.a * o.a
         t1 = s.b * o.b
         t2 = (s.a + s.b) * (o.a + o.b)
@@ -135,6 +179,14 @@ class F2:
 
     def conj(s):
         return F2(s.a, -s.b)
+
+    def is_zero(s):
+        return s.a.is_zero() and s.b.is_zero()
+
+
+def f2c(c, v):
+    """Fp2 constant from a (c0, c1) tuple of ints."""
+    return F2(const(c, v[0]), const(c, v[1]))
 
 
 class F6:
@@ -162,8 +214,20 @@ class F6:
         c2 = (a0 + a2) * (b0 + b2) - t0 - t2 + t1
         return F6(c0, c1, c2)
 
+    def sqr(s):  # Chung-Hasan SQR2
+        a0, a1, a2 = s.c
+        s0 = a0.sqr()
+        s1 = (a0 * a1).smul(2)
+        s2 = (a0 - a1 + a2).sqr()
+        s3 = (a1 * a2).smul(2)
+        s4 = a2.sqr()
+        return F6(s0 + s3.mul_xi(), s1 + s4.mul_xi(), s1 + s2 + s3 - s0 - s4)
+
     def mul_v(s):
         return F6(s.c[2].mul_xi(), s.c[0], s.c[1])
+
+    def mul_f2(s, k):
+        return F6(*(x * k for x in s.c))
 
     def mul_01(s, b0, b1):
         a0, a1, a2 = s.c
@@ -189,6 +253,26 @@ class F12:
         t = s.c0 * s.c1
         c0 = (s.c0 + s.c1) * (s.c0 + s.c1.mul_v()) - t - t.mul_v()
         return F12(c0, t.smul(2))
+
+    def cyc_sqr(s):
+        """Granger-Scott squaring, valid in the cyclotomic subgroup: 6 Fp2 products."""
+        z0, z4, z3 = s.c0.c
+        z2, z1, z5 = s.c1.c
+
+        def fp4_sqr(a, b):  # (a + b y)^2, y^2 = xi
+            t = a * b
+            return (a + b) * (a + b.mul_xi()) - t - t.mul_xi(), t.smul(2)
+
+        t0, t1 = fp4_sqr(z0, z1)
+        t2, t3 = fp4_sqr(z2, z3)
+        t4, t5 = fp4_sqr(z4, z5)
+        z0 = t0.smul(3) - z0.smul(2)
+        z1 = t1.smul(3) + z1.smul(2)
+        z2 = t5.mul_xi().smul(3) + z2.smul(2)
+        z3 = t4.smul(3) - z3.smul(2)
+        z4 = t2.smul(3) - z4.smul(2)
+        z5 = t3.smul(3) + z5.smul(2)
+        return F12(F6(z0, z4, z3), F6(z2, z1, z5))
 
     def conj(s):
         return F12(s.c0, -s.c1)
@@ -219,6 +303,177 @@ def f2_from_frame(c, frame, off):
 
 
 # --------------------------------------------------------------------------
+# field constants (computed here so the tool stays standalone)
+# --------------------------------------------------------------------------
+
+
+def _f2mul(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+def _f2pow(a, e):
+    r = (1, 0)
+    while e:
+        if e & 1:
+            r = _f2mul(r, a)
+        a = _f2mul(a, a)
+        e >>= 1
+    return r
+
+
+def _f2inv(a):
+    n = pow((a[0] * a[0] + a[1] * a[1]) % P, P - 2, P)
+    return (a[0] * n % P, (-a[1]) * n % P)
+
+
+XI = (1, 1)
+PSI_CX = _f2inv(_f2pow(XI, (P - 1) // 3))
+PSI_CY = _f2inv(_f2pow(XI, (P - 1) // 2))
+GAMMA1 = [_f2pow(XI, k * (P - 1) // 6) for k in range(6)]
+GAMMA2 = [_f2mul(_f2pow(XI, k * (P - 1) // 6), _f2pow(XI, k * (P - 1) // 6 * P)) for k in range(6)]
+B2_3 = (12, 12)  # 3 * b for E2: b = 4(1 + i)
+B1_3 = 12        # 3 * b for E1: b = 4
+# 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3), coefficients c0 + c1 i
+ISO_XNUM = [
+    (0x5C759507E8E333EBB5B7A9A47D7ED8532C52D39FD3A042A88B58423C50AE15D5C2638E343D9C71C6238AAAAAAAA97D6,
+     0x5C759507E8E333EBB5B7A9A47D7ED8532C52D39FD3A042A88B58423C50AE15D5C2638E343D9C71C6238AAAAAAAA97D6),
+    (0, 0x11560BF17BAA99BC32126FCED787C88F984F87ADF7AE0C7F9A208C6B4F20A4181472AAA9CB8D555526A9FFFFFFFFC71A),
+    (0x11560BF17BAA99BC32126FCED787C88F984F87ADF7AE0C7F9A208C6B4F20A4181472AAA9CB8D555526A9FFFFFFFFC71E,
+     0x8AB05F8BDD54CDE190937E76BC3E447CC27C3D6FBD7063FCD104635A790520C0A395554E5C6AAAA9354FFFFFFFFE38D),
+    (0x171D6541FA38CCFAED6DEA691F5FB614CB14B4E7F4E810AA22D6108F142B85757098E38D0F671C7188E2AAAAAAAA5ED1, 0),
+]
+ISO_XDEN = [
+    (0, 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAA63),
+    (0xC, 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAA9F),
+    (1, 0),
+]
+ISO_YNUM = [
+    (0x1530477C7AB4113B59A4C18B076D11930F7DA5D4A07F649BF54439D87D27E500FC8C25EBF8C92F6812CFC71C71C6D706,
+     0x1530477C7AB4113B59A4C18B076D11930F7DA5D4A07F649BF54439D87D27E500FC8C25EBF8C92F6812CFC71C71C6D706),
+    (0, 0x5C759507E8E333EBB5B7A9A47D7ED8532C52D39FD3A042A88B58423C50AE15D5C2638E343D9C71C6238AAAAAAAA97BE),
+    (0x11560BF17BAA99BC32126FCED787C88F984F87ADF7AE0C7F9A208C6B4F20A4181472AAA9CB8D555526A9FFFFFFFFC71C,
+     0x8AB05F8BDD54CDE190937E76BC3E447CC27C3D6FBD7063FCD104635A790520C0A395554E5C6AAAA9354FFFFFFFFE38F),
+    (0x124C9AD43B6CF79BFBF7043DE3811AD0761B0F37A1E26286B0E977C69AA274524E79097A56DC4BD9E1B371C71C718B10, 0),
+]
+ISO_YDEN = [
+    (0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFA8FB,
+     0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFA8FB),
+    (0, 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFA9D3),
+    (0x12, 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAA99),
+    (1, 0),
+]
+
+# --------------------------------------------------------------------------
+# complete projective point arithmetic on y^2 = x^3 + b (a = 0):
+# Renes-Costello-Batina 2016, algorithms 7 (add), 8 (mixed add), 9 (double).
+# Exception-free: the identity is (0 : 1 : 0) and every input is handled, so
+# a wave program needs no branches.  Works over Fp (E1) and Fp2 (E2); b3 =
+# 3b enters only linearly (12 and 12(1+i)).
+# --------------------------------------------------------------------------
+
+
+def _mulb3(t, b3):
+    if isinstance(t, F2):  # 12(1+i) * (a + b i) = 12(a - b) + 12(a + b) i
+        return F2((t.a - t.b).smul(b3[0]), (t.a + t.b).smul(b3[0]))
+    return t.smul(b3)
+
+
+def rcb_add(P1, P2, b3):
+    X1, Y1, Z1 = P1
+    X2, Y2, Z2 = P2
+    t0, t1, t2 = X1 * X2, Y1 * Y2, Z1 * Z2
+    t3 = (X1 + Y1) * (X2 + Y2) - t0 - t1
+    t4 = (Y1 + Z1) * (Y2 + Z2) - t1 - t2
+    y3 = (X1 + Z1) * (X2 + Z2) - t0 - t2
+    t0 = t0.smul(3)
+    t2 = _mulb3(t2, b3)
+    z3 = t1 + t2
+    t1 = t1 - t2
+    y3 = _mulb3(y3, b3)
+    X3 = t3 * t1 - t4 * y3
+    Y3 = t1 * z3 + y3 * t0
+    Z3 = z3 * t4 + t0 * t3
+    return (X3, Y3, Z3)
+
+
+def rcb_add_aff(P1, Q, b3):
+    """P1 projective + Q affine (Q must not be the identity)."""
+    X1, Y1, Z1 = P1
+    X2, Y2 = Q
+    t0, t1 = X1 * X2, Y1 * Y2
+    t3 = (X1 + Y1) * (X2 + Y2) - t0 - t1
+    t4 = Y2 * Z1 + Y1
+    y3 = X2 * Z1 + X1
+    t0 = t0.smul(3)
+    t2 = _mulb3(Z1, b3)
+    z3 = t1 + t2
+    t1 = t1 - t2
+    y3 = _mulb3(y3, b3)
+    X3 = t3 * t1 - t4 * y3
+    Y3 = t1 * z3 + y3 * t0
+    Z3 = z3 * t4 + t0 * t3
+    return (X3, Y3, Z3)
+
+
+def rcb_dbl(P1, b3):
+    X, Y, Z = P1
+    t0 = Y.sqr() if isinstance(Y, F2) else Y * Y
+    t1 = Y * Z
+    t2 = _mulb3(Z.sqr() if isinstance(Z, F2) else Z * Z, b3)
+    u = X * Y
+    z8 = t0.smul(8)
+    X3a = t2 * z8
+    Z3 = t1 * z8
+    w = t0 - t2.smul(3)
+    Y3 = w * (t0 + t2) + X3a
+    X3 = (w * u).smul(2)
+    return (X3, Y3, Z3)
+
+
+def pt_from_frame(c, frame, off, ext):
+    if ext:
+        return tuple(f2_from_frame(c, frame, off + 2 * k) for k in range(3))
+    return tuple(inp(c, frame, off + k) for k in range(3))
+
+
+def pt_out(pt):
+    out = []
+    for v in pt:
+        out += [v.a, v.b] if isinstance(v, F2) else [v]
+    return out
+
+
+def g2_psi_proj(c, pt):
+    X, Y, Z = pt
+    return (X.conj() * f2c(c, PSI_CX), Y.conj() * f2c(c, PSI_CY), Z.conj())
+
+
+def g2_psi2_proj(c, pt):
+    cx = _f2mul(PSI_CX, (PSI_CX[0], (-PSI_CX[1]) % P))
+    cy = _f2mul(PSI_CY, (PSI_CY[0], (-PSI_CY[1]) % P))
+    X, Y, Z = pt
+    return (X * f2c(c, cx), Y * f2c(c, cy), Z)
+
+
+def neg_pt(pt):
+    return (pt[0], -pt[1], pt[2])
+
+
+def xabs_runs():
+    """Square-and-multiply schedule of |x| after the leading bit: list of
+    (doublings, add_after)."""
+    runs, k = [], 0
+    for i in range(62, -1, -1):
+        k += 1
+        if (X_ABS >> i) & 1:
+            runs.append((k, True))
+            k = 0
+    if k:
+        runs.append((k, False))
+    return runs
+
+
+# --------------------------------------------------------------------------
 # programs
 # --------------------------------------------------------------------------
 
@@ -232,6 +487,42 @@ def prog_fp12_mul(c):
 def prog_fp12_sqr(c):
     a = f12_from_frame(c, 0)
     return {1: a.sqr().coeffs()}
+
+
+def make_cyc_run(k, mul):
+    """frame 0: a, frame 1: base (multiplier), frame 2: out = a^(2^k) [* base]."""
+
+    def prog(c):
+        a = f12_from_frame(c, 0)
+        for j in range(k):
+            a = a.cyc_sqr()
+            if j + 1 < k or mul:
+                a = mat12(a)
+        if mul:
+            a = a * f12_from_frame(c, 1)
+        return {2: a.coeffs()}
+
+    return prog
+
+
+def prog_fp12_frob(n):
+    """frame 0: a, frame 1: out = a^(p^n): w-basis coefficient k becomes
+    conj^n(c_k) * xi^(k (p^n - 1) / 6)."""
+
+    def prog(c):
+        v = [inp(c, 0, i) for i in range(12)]
+        out = []
+        for k in range(6):
+            x = F2(v[2 * k], v[2 * k + 1])
+            if n % 2 == 1:
+                x = x.conj()
+            g = _f2pow(XI, k * (P ** n - 1) // 6)
+            if g != (1, 0):
+                x = x * f2c(c, g)
+            out += [x.a, x.b]
+        return {1: out}
+
+    return prog
 
 
 def _ml_line_dbl(c, T, nxP, yP):
@@ -313,50 +604,231 @@ def prog_ml_add(c):
     return {0: f.mul_line(l0, l2, l3).coeffs(), 1: _t_out(T2)}
 
 
+# ---- curve programs (projective, complete) -------------------------------
+
+
+def make_xmul_run(ext, k, add):
+    """frame 0: R (projective), frame 1: base (projective), frame 2: out = [2^k] R (+ base)."""
+    b3 = B2_3 if ext else B1_3
+
+    def prog(c):
+        R = pt_from_frame(c, 0, 0, ext)
+        for _ in range(k):
+            R = rcb_dbl(R, b3)
+        if add:
+            R = rcb_add(R, pt_from_frame(c, 1, 0, ext), b3)
+        return {2: pt_out(R)}
+
+    return prog
+
+
+def make_pt_add(ext):
+    """frame 0: A, frame 1: B, frame 2: out = A + B (projective)."""
+    b3 = B2_3 if ext else B1_3
+
+    def prog(c):
+        return {2: pt_out(rcb_add(pt_from_frame(c, 0, 0, ext), pt_from_frame(c, 1, 0, ext), b3))}
+
+    return prog
+
+
+def make_dbl_add_sel(ext):
+    """Double-and-always-add step with a per-item select:
+    frame 0: R (projective, updated in place), frame 1: Q (affine x, y);
+    R <- pred ? 2R + Q : 2R."""
+    b3 = B2_3 if ext else B1_3
+
+    def prog(c):
+        R = pt_from_frame(c, 0, 0, ext)
+        if ext:
+            Q = (f2_from_frame(c, 1, 0), f2_from_frame(c, 1, 2))
+        else:
+            Q = (inp(c, 1, 0), inp(c, 1, 1))
+        D = rcb_dbl(R, b3)
+        S = rcb_add_aff(D, Q, b3)
+        outs = [sel(c, s, d) for s, d in zip(pt_out(S), pt_out(D))]
+        return {0: outs}
+
+    return prog
+
+
+def prog_g2_aff_to_proj_psi_check(c):
+    """Subgroup check inputs/outputs for sigma: frame 0: sigma affine (x, y);
+    frame 1: M = [|x|] sigma (projective).  Output frame 2: the three values
+    X_psi Z_M - X_M Z_psi, Y_psi Z_M + Y_M Z_psi (Fp2 each) and Z_M; sigma
+    is in G2 iff psi(sigma) == -M, i.e. the first two are zero and Z_M != 0."""
+    S = (f2_from_frame(c, 0, 0), f2_from_frame(c, 0, 2), F2(const(c, 1), zero(c)))
+    Xp, Yp, Zp = g2_psi_proj(c, S)
+    M = pt_from_frame(c, 1, 0, True)
+    dx = Xp * M[2] - M[0] * Zp
+    dy = Yp * M[2] + M[1] * Zp
+    return {2: [dx.a, dx.b, dy.a, dy.b, M[2].a, M[2].b]}
+
+
+def prog_iso_pair(c):
+    """3-isogeny of the two SSWU outputs and their sum on E2.
+    frame 0: (x0, y0, x1, y1) affine on E2' (8 Fp); frame 1: out projective
+    Q = iso(P0) + iso(P1) (6 Fp)."""
+    pts = []
+    for k in range(2):
+        x, y = f2_from_frame(c, 0, 4 * k), f2_from_frame(c, 0, 4 * k + 2)
+        xx = x.sqr()
+        xxx = xx * x
+
+        def poly(coefs, has_x3_one=False):
+            acc = f2c(c, coefs[0])
+            terms = [x, xx, xxx]
+            for j in range(1, len(coefs)):
+                if coefs[j] == (1, 0):
+                    acc = acc + terms[j - 1]
+                elif coefs[j] != (0, 0):
+                    acc = acc + terms[j - 1] * f2c(c, coefs[j])
+            return acc
+
+        xnum, xden, ynum, yden = poly(ISO_XNUM), poly(ISO_XDEN), poly(ISO_YNUM), poly(ISO_YDEN)
+        # (xnum/xden, y ynum/yden) -> projective (xnum yden : y ynum xden : xden yden)
+        pts.append((xnum * yden, (y * ynum) * xden, xden * yden))
+    return {1: pt_out(rcb_add(pts[0], pts[1], B2_3))}
+
+
+def prog_clear_pre(c):
+    """Cofactor clearing, part 1 (Budroni-Pintore).  frame 0: P; frame 1:
+    M1 = [|x|] P.  Outputs frame 2: A = t1 + psi(P) where t1 = -M1 (the
+    input of the second [|x|] multiplication) and frame 3: C = psi^2(2P) -
+    psi(P) - t1 - P  (so h_eff P = C - [|x|] A)."""
+    Pp = pt_from_frame(c, 0, 0, True)
+    M1 = pt_from_frame(c, 1, 0, True)
+    t1 = neg_pt(M1)
+    t2 = g2_psi_proj(c, Pp)
+    t3 = g2_psi2_proj(c, rcb_dbl(Pp, B2_3))
+    A = rcb_add(t1, t2, B2_3)
+    Cc = rcb_add(rcb_add(t3, neg_pt(t2), B2_3), rcb_add(M1, neg_pt(Pp), B2_3), B2_3)
+    return {2: pt_out(A), 3: pt_out(Cc)}
+
+
+def prog_clear_post(c):
+    """frame 0: C, frame 1: M2 = [|x|] A; out frame 2: C - M2."""
+    return {2: pt_out(rcb_add(pt_from_frame(c, 0, 0, True), neg_pt(pt_from_frame(c, 1, 0, True)), B2_3))}
+
+
+def prog_proj_to_aff2(c):
+    """frame 0: projective (X, Y, Z) over Fp2, frame 1: zi = 1/Z (Fp2);
+    out frame 2: (x, y) affine."""
+    X, Y, Z = pt_from_frame(c, 0, 0, True)
+    zi = f2_from_frame(c, 1, 0)
+    x, y = X * zi, Y * zi
+    return {2: [x.a, x.b, y.a, y.b]}
+
+
+def prog_proj_to_aff1(c):
+    X, Y, Z = pt_from_frame(c, 0, 0, False)
+    zi = inp(c, 1, 0)
+    return {2: [X * zi, Y * zi]}
+
+
+def prog_fp2_norm(c):
+    """frame 0: a (Fp2); out frame 1: a0^2 + a1^2 (Fp)."""
+    a = f2_from_frame(c, 0, 0)
+    return {1: [a.a * a.a + a.b * a.b]}
+
+
+def prog_fp2_inv_finish(c):
+    """frame 0: a (Fp2), frame 1: n = 1/norm(a); out frame 2: a^-1 = conj(a) n."""
+    a = f2_from_frame(c, 0, 0)
+    n = inp(c, 1, 0)
+    return {2: [a.a * n, -(a.b * n)]}
+
+
+X_RUNS = xabs_runs()
+
 PROGRAMS = {
     # name: (builder, frame sizes (excluding scratch))
-    "FP12_MUL": (prog_fp12_mul, [12, 12, 12]),
+    "FP12_MUL": (prog_fp12_mul, [12, 12, 12], {2: 0}),
     "FP12_SQR": (prog_fp12_sqr, [12, 12]),
+    "FP12_FROB1": (prog_fp12_frob(1), [12, 12]),
+    "FP12_FROB2": (prog_fp12_frob(2), [12, 12]),
     "ML_DBL": (prog_ml_dbl, [12, 6, 2, 4]),
     "ML_DBL_FIRST": (prog_ml_dbl_first, [12, 6, 2, 4]),
     "ML_ADD": (prog_ml_add, [12, 6, 2, 4]),
+    "G2_ADD": (make_pt_add(True), [6, 6, 6]),
+    "G1_ADD": (make_pt_add(False), [3, 3, 3]),
+    "G1_DAS": (make_dbl_add_sel(False), [3, 2]),
+    "G2_DAS": (make_dbl_add_sel(True), [6, 4]),
+    "G2_SUBCHK": (prog_g2_aff_to_proj_psi_check, [4, 6, 6]),
+    "ISO_PAIR": (prog_iso_pair, [8, 6]),
+    "CLEAR_PRE": (prog_clear_pre, [6, 6, 6, 6]),
+    "CLEAR_POST": (prog_clear_post, [6, 6, 6]),
+    "G2_TOAFF": (prog_proj_to_aff2, [6, 2, 4]),
+    "G1_TOAFF": (prog_proj_to_aff1, [3, 1, 2]),
+    "FP2_NORM": (prog_fp2_norm, [2, 1]),
+    "FP2_INVFIN": (prog_fp2_inv_finish, [2, 1, 2]),
 }
+for _k, _add in X_RUNS:
+    # the output frame may alias the running value (in-place runs)
+    PROGRAMS[f"CYC_{_k}{'M' if _add else ''}"] = (make_cyc_run(_k, _add), [12, 12, 12], {2: 0})
+    PROGRAMS[f"G2X_{_k}{'A' if _add else ''}"] = (make_xmul_run(True, _k, _add), [6, 6, 6], {2: 0})
 
 # --------------------------------------------------------------------------
 # compiler: level scheduling, slot assignment, table emission
 # --------------------------------------------------------------------------
-LANES = 64
-MAX_TERMS = 40  # per operand (padded); asserted
-MAX_COEF = 31
+MAX_TERMS = 12  # per operand (after splitting)
+MAX_COEF = 127
+MAX_MAG = 190  # sum of |coefficients| per accumulated form (the 256 p offset bounds it)
+SPLIT = 12  # linear combinations longer than this are summed as a tree of partial sums
+CONST_POOL: dict = {}  # canonical value -> pool index (shared by all programs)
 
 
-SPLIT = 8  # linear combinations longer than this are summed as a tree of partial sums
+def _pool_index(v):
+    if v not in CONST_POOL:
+        CONST_POOL[v] = len(CONST_POOL)
+    return CONST_POOL[v]
 
 
-def compile_program(name, builder, frames):
+def compile_program(name, builder, frames, alias=None):
+    alias = alias or {}
+
+    def canon(key):
+        return (alias.get(key[0], key[0]), key[1])
+
     c = Ctx()
     outputs = builder(c)  # {frame: [V...]}
-    nframes = len(frames)
-    scratch_frame = nframes
-    out_list = [(fr, i, v) for fr, vs in outputs.items() for i, v in enumerate(vs)]
+    scratch_frame = len(frames)
+    assert scratch_frame < CONST_FRAME
+    out_list = [(fr, i, v.f) for fr, vs in outputs.items() for i, v in enumerate(vs)]
 
-    # atoms reachable from the outputs
+    def deps(a):
+        d = c.atoms[a]
+        if d[0] in ("prod", "sel"):
+            return list(d[1]) + list(d[2])
+        if d[0] == "lin":
+            return list(d[1])
+        return []
+
     need = set()
-    stack = [a for _, _, v in out_list for a in v.f]
+    stack = [a for _, _, f in out_list for a in f]
     while stack:
         a = stack.pop()
         if a in need:
             continue
         need.add(a)
-        d = c.atoms[a]
-        if d[0] == "prod":
-            stack += list(d[1]) + list(d[2])
+        stack += deps(a)
 
-    # split long linear forms into partial-sum atoms ('lin', form)
+    def chunked(items):
+        chunks, cur, mag = [], [], 0
+        for a, k in items:
+            if cur and (len(cur) >= SPLIT or mag + abs(k) > MAX_MAG):
+                chunks.append(dict(cur))
+                cur, mag = [], 0
+            cur.append((a, k))
+            mag += abs(k)
+        if cur:
+            chunks.append(dict(cur))
+        return chunks
+
     def shrink(form):
         items = sorted(form.items())
-        while len(items) > SPLIT:
-            chunks = [dict(items[k:k + SPLIT]) for k in range(0, len(items), SPLIT)]
+        while len(items) > SPLIT or sum(abs(k) for _, k in items) > MAX_MAG:
+            chunks = chunked(items)
             items = []
             for ch in chunks:
                 if len(ch) == 1:
@@ -367,47 +839,84 @@ def compile_program(name, builder, frames):
                     items.append((a, 1))
         return dict(items)
 
-    prods = sorted(a for a in need if c.atoms[a][0] == "prod")
-    for a in prods:
-        _, fa, fb = c.atoms[a]
-        c.atoms[a] = ("prod", shrink(fa), shrink(fb))
-    out_list = [(fr, i, shrink(v.f)) for fr, i, v in out_list]
+    for a in sorted(a for a in need if c.atoms[a][0] in ("prod", "sel")):
+        k, fa, fb = c.atoms[a]
+        c.atoms[a] = (k, shrink(fa), shrink(fb))
+    out_list = [(fr, i, shrink(f)) for fr, i, f in out_list]
 
     level = {}
 
-    def deps(a):
-        d = c.atoms[a]
-        if d[0] == "prod":
-            return list(d[1]) + list(d[2])
-        if d[0] == "lin":
-            return list(d[1])
-        return []
-
     def lvl(a):
         if a not in level:
-            ds = deps(a)
-            level[a] = 0 if c.atoms[a][0] in ("in", "const") else 1 + max([lvl(x) for x in ds] or [0])
+            if c.atoms[a][0] in ("in", "const"):
+                level[a] = 0
+            else:
+                level[a] = 1 + max([lvl(x) for x in deps(a)] or [0])
         return level[a]
 
-    work = [a for a in need if c.atoms[a][0] in ("prod", "lin")]
+    work = [a for a in need if c.atoms[a][0] in ("prod", "lin", "sel", "lut")]
     for a in work:
         lvl(a)
-    depth = max([level[a] for a in work] or [0])
-    out_level = 1 + max([depth] + [max([level[a] for a in f] or [0]) for _, _, f in out_list])
-    consts = sorted(a for a in need if c.atoms[a][0] == "const")
+    # last level at which each input slot is read
+    last_read = defaultdict(int)
+    for a in work:
+        d = c.atoms[a]
+        srcs = deps(a)
+        for s in srcs:
+            if c.atoms[s][0] == "in":
+                key = canon((c.atoms[s][1], c.atoms[s][2]))
+                last_read[key] = max(last_read[key], level[a])
+        if d[0] == "lut":
+            for j in range(16):
+                key = canon((d[1], d[2] + j * d[3]))
+                last_read[key] = max(last_read[key], level[a])
     slot = {}
     for a in need:
         d = c.atoms[a]
         if d[0] == "in":
             slot[a] = (d[1], d[2])
-    sidx = 0
-    for a in consts:
-        slot[a] = (scratch_frame, sidx)
-        sidx += 1
+        elif d[0] == "const":
+            slot[a] = (CONST_FRAME, _pool_index(d[1]))
+    # outputs: direct write of an op result when safe, else a lin item
+    out_items = []
+    direct = {}
+    for fr, i, f in out_list:
+        key = (fr, i)
+        ck = canon(key)
+        if len(f) == 1:
+            (a, k), = f.items()
+            if k == 1 and c.atoms[a][0] in ("prod", "sel", "lut") and a not in direct \
+                    and last_read.get(ck, 0) < level[a] and key not in direct.values():
+                direct[a] = key
+                continue
+        lvl_o = 1 + max([lvl(a) for a in f] or [0])
+        lvl_o = max(lvl_o, last_read.get(ck, 0) + 1)
+        out_items.append((lvl_o, key, f))
+    for a, key in direct.items():
+        slot[a] = key
+    # scratch slots by liveness: a slot is reused once every reader of its
+    # previous value ran at an earlier level (reads and writes of one level
+    # may interleave across the passes of a multi-item level)
+    last_use = defaultdict(int)
+    for a in work:
+        for s_ in deps(a):
+            last_use[s_] = max(last_use[s_], level[a])
+    for lv_o, _, f in out_items:
+        for s_ in f:
+            last_use[s_] = max(last_use[s_], lv_o)
+    occupied = []  # [last_use_level, slot]
     for a in sorted(work, key=lambda a: (level[a], a)):
-        slot[a] = (scratch_frame, sidx)
-        sidx += 1
-    scratch_size = sidx
+        if a in slot:
+            continue
+        for ent in occupied:
+            if ent[0] < level[a]:
+                slot[a] = (scratch_frame, ent[1])
+                ent[0] = last_use[a]
+                break
+        else:
+            slot[a] = (scratch_frame, len(occupied))
+            occupied.append([last_use[a], len(occupied)])
+    scratch_size = len(occupied)
 
     def terms(form):
         ts = []
@@ -425,77 +934,177 @@ def compile_program(name, builder, frames):
         d = c.atoms[a]
         if d[0] == "prod":
             by_level[level[a]].append(("mul", slot[a], terms(d[1]), terms(d[2])))
+        elif d[0] == "sel":
+            by_level[level[a]].append(("sel", slot[a], terms(d[1]), terms(d[2])))
+        elif d[0] == "lut":
+            by_level[level[a]].append(("lut", slot[a], [(d[1], d[2], d[3])], []))
         else:
             by_level[level[a]].append(("lin", slot[a], terms(d[1]), []))
-    for fr, i, f in out_list:  # outputs last: every read of an input frame happens before
-        by_level[out_level].append(("lin", (fr, i), terms(f), []))
+    for lv, key, f in out_items:
+        by_level[lv].append(("lin", key, terms(f), []))
+    order = {"mul": 0, "sel": 1, "lut": 2, "lin": 3}
     levels = []
     for L in sorted(by_level):
         its = by_level[L]
-        its.sort(key=lambda t: t[0] != "mul")  # products first (lanes 0..)
-        for k in range(0, len(its), LANES):
-            levels.append(its[k:k + LANES])
+        its.sort(key=lambda t: (order[t[0]], -(len(t[2]) + len(t[3]))))
+        levels.append(its)
+    # hazard check: every write of an input-frame slot happens at a level
+    # after the last read of that slot's input value
+    writes = {}
+    for L in sorted(by_level):
+        for kind, dst, a, b in by_level[L]:
+            assert dst not in writes or dst[0] == scratch_frame, (name, dst)
+            writes[dst] = L
+            if dst[0] != scratch_frame:
+                assert last_read.get(canon(dst), -1) < L, (name, dst, L)
     nprod = sum(1 for a in work if c.atoms[a][0] == "prod")
-    return {"name": name, "frames": frames + [scratch_size], "levels": levels,
-            "consts": [(slot[a][1], c.atoms[a][1]) for a in consts],
-            "nprod": nprod, "depth": depth}
+    return {"name": name, "frames": frames + [scratch_size], "levels": levels, "nprod": nprod,
+            "written": sorted(outputs) + [scratch_frame],
+            "depth": max([level[a] for a in work] or [0])}
 
 
-def pack_term(fr, ix, k):
-    # 32 bits: frame (4) | index (12) | coef + 128 (8); 0 means "no term"
-    assert 0 <= fr < 16 and 0 <= ix < 4096 and -MAX_COEF <= k <= MAX_COEF and k != 0
-    return (fr << 20) | (ix << 8) | (k + 128)
+# --------------------------------------------------------------------------
+# binding: a program instance places its frames at fixed slot offsets of the
+# item region, so table words carry absolute slot indices.
+#   term word: [31:24] coef + 128 (lut: stride + 128) | [23] const pool | [22:0] slot
+#   dest word: [31:30] kind | [22:0] slot
+# --------------------------------------------------------------------------
+LAYOUT = {}      # layout name -> {"stride": n, "consts": {...}} (emitted as C++ constants)
+INSTANCES = []   # (instance name, program name, frame bases, scratch base)
+
+
+def layout(name, **slots):
+    LAYOUT[name] = slots
+
+
+def instance(iname, prog, bases, scratch):
+    INSTANCES.append((iname, prog, list(bases), scratch))
+
+
+def bind(p, bases, scratch, alias):
+    nfr = len(p["frames"]) - 1
+    assert len(bases) == nfr, (p["name"], bases)
+    sizes = p["frames"][:-1]
+    rng_ = [(bases[i], bases[i] + sizes[i]) for i in range(nfr)] + [(scratch, scratch + p["frames"][-1])]
+    for i in range(nfr + 1):
+        for j in range(i + 1, nfr + 1):
+            (a0, a1), (b0, b1) = rng_[i], rng_[j]
+            if a0 < b1 and b0 < a1 and (i in p["written"] or j in p["written"]):
+                # overlap with a written frame: only a declared alias with identical placement
+                ok = (alias.get(i) == j or alias.get(j) == i) and a0 == b0
+                assert ok, (p["name"], "frames", i, j, "overlap", bases, scratch)
+
+    def slot_of(fr, ix):
+        if fr == CONST_FRAME:
+            return (1 << 23) | ix
+        b = scratch if fr == nfr else bases[fr]
+        return b + ix
+
+    levels = []
+    for items in p["levels"]:
+        bl = []
+        for kind, (fr, ix), a, b in items:
+            d = (KIND[kind] << 30) | slot_of(fr, ix)
+            if kind == "lut":
+                (tf, ti, ts), = a
+                ta = [((ts + 128) << 24) | slot_of(tf, ti)]
+            else:
+                ta = [((k + 128) << 24) | slot_of(f, i) for f, i, k in a]
+            tb = [((k + 128) << 24) | slot_of(f, i) for f, i, k in b]
+            bl.append((d, ta, tb))
+        levels.append(bl)
+    return levels
 
 
 def emit(progs, path):
+    by_name = {p["name"]: p for p in progs}
     out = ["// GENERATED by tools/wavec.py -- do not edit.",
-           "// Wave programs: levels of independent Montgomery products whose operands are",
-           "// small-integer linear combinations of slots (see bls_wave.h).",
+           "// Wave program instances: levels of independent Montgomery products / linear ops",
+           "// whose operands are small-integer linear combinations of slots (see bls_vm.h).",
            "#pragma once", "#include <stdint.h>", "", "namespace bls {", ""]
+    for lname, vals in LAYOUT.items():
+        for k, v in vals.items():
+            out.append(f"static constexpr int WL_{lname}_{k} = {v};")
+    out.append("")
     for p in progs:
-        nm = p["name"]
-        lv_desc = []
-        tbl = []
-        for items in p["levels"]:
-            na = max(len(a) for _, _, a, _ in items)
-            nb = max(len(b) for _, _, _, b in items)
-            stride = 1 + na + nb
+        out.append(f"static constexpr int WP_{p['name']}_SCRATCH = {p['frames'][-1]};")
+    out.append("")
+    for iname, pname, bases, scratch in INSTANCES:
+        p = by_name[pname]
+        lv_desc, tbl = [], []
+        for items in bind(p, bases, scratch, PROGRAMS[pname][2] if len(PROGRAMS[pname]) > 2 else {}):
+            na = max(len(a) for _, a, _ in items)
+            nb = max(len(b) for _, _, b in items)
             base = len(tbl)
-            for kind, (fr, ix), a, b in items:
-                tbl.append((1 << 31 if kind == "mul" else 0) | (fr << 20) | (ix << 8))  # destination word
-                ta = [pack_term(*t) for t in a] + [0] * (na - len(a))
-                tb = [pack_term(*t) for t in b] + [0] * (nb - len(b))
-                tbl += ta + tb
-            lv_desc.append((0, len(items), na, nb, base))
-        out.append(f"// {nm}: frames {p['frames']} (last = scratch), {p['nprod']} products, depth {p['depth']}, "
-                   f"{len(p['levels'])} levels")
-        out.append(f"static constexpr uint32_t WP_{nm}_TERMS[{len(tbl)}] = {{{', '.join(str(x) for x in tbl)}}};")
-        out.append(f"static constexpr uint32_t WP_{nm}_LEVELS[{len(lv_desc)}][5] = {{"
-                   + ", ".join("{%d, %d, %d, %d, %d}" % d for d in lv_desc) + "};")
-        out.append(f"static constexpr int WP_{nm}_NLEVELS = {len(lv_desc)};")
-        out.append(f"static constexpr int WP_{nm}_SCRATCH = {p['frames'][-1]};")
-        cs = p["consts"]
-        out.append(f"static constexpr int WP_{nm}_NCONST = {len(cs)};")
-        if cs:
-            out.append(f"static constexpr uint32_t WP_{nm}_CONSTS[{len(cs)}][13] = {{"
-                       + ", ".join("{%d, %s}" % (ix, ", ".join("0x%08xu" % ((v * (1 << 406) % P) >> (32 * i) & 0xFFFFFFFF)
-                                                             for i in range(12))) for ix, v in cs) + "};")
+            for d, ta, tb in items:
+                tbl.append(d)
+                tbl += ta + [0] * (na - len(ta)) + tb + [0] * (nb - len(tb))
+            lv_desc.append((len(items), na, nb, base))
+        out.append(f"// {iname} = {pname} at frames {bases}, scratch {scratch}: {p['nprod']} products, "
+                   f"{len(lv_desc)} levels")
+        out.append(f"static constexpr uint32_t WP_{iname}_TERMS[{len(tbl)}] = {{{', '.join(str(x) for x in tbl)}}};")
+        out.append(f"static constexpr uint32_t WP_{iname}_LEVELS[{len(lv_desc)}][4] = {{"
+                   + ", ".join("{%d, %d, %d, %d}" % d for d in lv_desc) + "};")
+        out.append(f"static constexpr int WP_{iname}_NLEVELS = {len(lv_desc)};")
         out.append("")
+    pool = sorted(CONST_POOL.items(), key=lambda kv: kv[1])
+    rows = []
+    for v, _ in pool:
+        m = v * (1 << 406) % P
+        rows.append("{{" + ", ".join("0x%08xu" % ((m >> (32 * i)) & 0xFFFFFFFF) for i in range(12)) + "}}")
+    out.append(f"static constexpr int WP_NCONST = {len(pool)};")
+    out.append("struct WpConst { uint32_t l[12]; };")
+    out.append(f"static constexpr WpConst WP_CONST_POOL[{max(1, len(pool))}] = {{{', '.join(rows or ['{{0}}'])}}};")
+    out.append("")
     out.append("}  // namespace bls")
     with open(path, "w") as fh:
         fh.write("\n".join(out) + "\n")
 
 
+def define_instances(progs):
+    """Slot layouts of the device kernels and the program instances they run."""
+    LAYOUT.clear()
+    INSTANCES.clear()
+    sc = {p["name"]: p["frames"][-1] for p in progs}
+    # Miller loop item region: f | T | P (-x, y) | Q | scratch
+    ml_s = max(sc["ML_DBL"], sc["ML_ADD"], sc["ML_DBL_FIRST"])
+    layout("ML", F=0, T=12, P=18, Q=20, S=24, STRIDE=24 + ml_s)
+    for nm in ("ML_DBL", "ML_ADD", "ML_DBL_FIRST"):
+        instance(nm, nm, [0, 12, 18, 20], 24)
+    # chunked Fp12 product: acc | in | scratch
+    layout("CH", STRIDE=24 + sc["FP12_MUL"])
+    instance("CH_MUL", "FP12_MUL", [0, 12, 0], 24)
+    # final exponentiation: registers R0..R6 (12 slots each) | scratch
+    cyc = [n for n in sc if n.startswith("CYC_")]
+    fe_s = max([sc["FP12_MUL"], sc["FP12_FROB1"], sc["FP12_FROB2"]] + [sc[n] for n in cyc])
+    layout("FE", NREG=7, S=84, STRIDE=84 + fe_s)
+    R = lambda k: 12 * k  # noqa: E731
+    for d, a, b in ((0, 0, 1), (0, 2, 1), (2, 2, 1), (2, 1, 3), (3, 3, 1), (1, 1, 4), (1, 1, 5)):
+        instance(f"FE_MUL_{d}{a}{b}", "FP12_MUL", [R(a), R(b), R(d)], 84)
+    instance("FE_FROB2_10", "FP12_FROB2", [R(0), R(1)], 84)
+    instance("FE_FROB2_43", "FP12_FROB2", [R(3), R(4)], 84)
+    instance("FE_FROB1_32", "FP12_FROB1", [R(2), R(3)], 84)
+    for i, (k, add) in enumerate(X_RUNS):  # pow_x: R1 = R2^|x|
+        nm = f"CYC_{k}{'M' if add else ''}"
+        cur = R(2) if i == 0 else R(1)
+        instance(f"FE_POWX_{i}", nm, [cur, R(2), R(1)], 84)
+    instance("FE_CUBE", "CYC_1M", [R(0), R(0), R(5)], 84)
+
+
 def compile_all():
-    return [compile_program(n, b, fr) for n, (b, fr) in PROGRAMS.items()]
+    CONST_POOL.clear()
+    progs = [compile_program(n, *spec) for n, spec in PROGRAMS.items()]
+    define_instances(progs)
+    return progs
 
 
 if __name__ == "__main__":
     progs = compile_all()
     for p in progs:
         sizes = [len(items) for items in p["levels"]]
-        print(f"{p['name']:14s} products={p['nprod']:4d} depth={p['depth']:2d} levels={len(p['levels'])} sizes={sizes} "
-              f"scratch={p['frames'][-1]}")
+        print(f"{p['name']:14s} products={p['nprod']:4d} depth={p['depth']:3d} levels={len(p['levels']):3d} "
+              f"scratch={p['frames'][-1]:4d} sizes={sizes if len(sizes) < 12 else sizes[:12] + ['...']}")
+    print("const pool:", len(CONST_POOL))
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "eth-consensus-specs_amd", "csrc",
                        "bls_waveprog.h")
     emit(progs, dst)
