@@ -43,7 +43,8 @@ def model_fme(n: int):
     """Per-item algorithmic work of FAV(n) with a resident registry."""
     return {
         "fav_gather": 11 * (n - 1),
-        "fav_sig": 1200 + 1200 + 1000 + 400,  # sig decode, G2 subgroup, RLC G1, RLC G2 (MSM share)
+        "sig_decode": 1200,             # signature decompression (Fp2 square root)
+        "sig_vm": 1200 + 1000 + 400,    # G2 subgroup check, RLC G1, RLC G2 (MSM share)
         "fav_hash": 6600,
         "miller": 4400,
     }

@@ -18,7 +18,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK,
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC,
   NSLOT
 };
 
@@ -52,8 +52,8 @@ struct bls_ctx {
   uint64_t prof_cnt[16] = {0};
 };
 
-static const char* const PROF_NAMES[] = {"fav_gather", "fav_sig", "fav_hash", "g2_sum", "sig_pair", "miller",
-                                         "fp12_prod", "final_exp", "fav_finish", "partials_prod"};
+static const char* const PROF_NAMES[] = {"fav_gather", "sig_decode", "fav_hash", "g2_sum",        "sig_pair", "miller",
+                                         "fp12_prod",  "final_exp",  "fav_finish", "partials_prod", "sig_vm"};
 static const int PROF_N = sizeof(PROF_NAMES) / sizeof(PROF_NAMES[0]);
 
 namespace {
@@ -580,12 +580,14 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     ctx->err = "no registry loaded";
     return BLS_E_NOREG;
   }
-  G1J *apk;
-  int* status;
+  G1J* apk;
+  int *status, *flag;
   G1A *apka, *rP;
   G2A *sig, *H;
   G2J *rS, *tmp, *S;
   Fp12 *f, *ft, *fo;
+  Fp* U;
+  uint64_t* rsc;
   uint8_t* d_seed;
   SCR(S_APK, B, apk);
   SCR(S_STATUS, B + 1, status);
@@ -594,6 +596,9 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_RP, B + 1, rP);
   SCR(S_RS, B, rS);
   SCR(S_H, B + 1, H);
+  SCR(S_U, 8 * B, U);
+  SCR(S_FLAG, B, flag);
+  SCR(S_RSC, B, rsc);
   SCR(S_G2J_T, 1024, tmp);
   SCR(S_G2J, 1, S);
   SCR(S_F, B + 1, f);
@@ -606,10 +611,11 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   // signature branch; both join before the Miller loops.
   HIPCK(hipEventRecord(ctx->ev_fork, st));
   HIPCK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-  PROF2(2, ctx->stream2, launch_fav_hash(ctx->stream2, B, d_msgs, nullptr, H));
+  PROF2(2, ctx->stream2, launch_h2c(ctx->stream2, B, d_msgs, nullptr, U, H, flag));
   HIPCK(hipEventRecord(ctx->ev_join, ctx->stream2));
   PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
-  PROF(1, launch_fav_sig(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rP, rS));
+  PROF(1, launch_sig_decode(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rsc));
+  PROF(10, launch_sig_vm(st, B, status, apka, sig, rsc, rP, rS));
   PROF(3, launch_g2_sum_jac(st, rS, B, tmp, S));
   PROF(4, launch_sig_pair(st, S, rP + B, H + B));
   HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));

@@ -1,0 +1,258 @@
+// FastAggregateVerify batch kernels, split by how the work parallelises:
+//   - lane kernels (one or two lanes per item) for the long sequential
+//     chains: SHA-256 expand, SSWU (square roots, inversions, Jacobi
+//     symbols), signature decompression, RLC scalars;
+//   - wave-program kernels (bls_vm.h, G items per 64-lane workgroup) for the
+//     point arithmetic: 3-isogeny + cofactor clearing of hash_to_G2, and the
+//     three signature-side chains ([|x|] sigma for the subgroup check,
+//     r * apk in G1, r * sigma in G2) advanced together one scalar bit per
+//     step with complete (exception-free) projective formulas.
+#include "bls_kernels.h"
+#include "bls_vm.h"
+
+namespace bls {
+
+__device__ static const uint8_t DST_POP_FAV[43] = {
+    'B', 'L', 'S', '_', 'S', 'I', 'G', '_', 'B', 'L', 'S', '1', '2', '3', '8', '1', 'G', '2', '_', 'X', 'M', 'D',
+    ':', 'S', 'H', 'A', '-', '2', '5', '6', '_', 'S', 'S', 'W', 'U', '_', 'R', 'O', '_', 'P', 'O', 'P', '_'};
+
+constexpr int FAV_G = 2;  // items per wave-program workgroup
+
+// ------------------------------------------------------------ hash_to_G2 --
+// (1) lane (item, t): expand_message_xmd + hash_to_field, then SSWU of u_t.
+// U[8 i + 4 t ..] = (x.c0, x.c1, y.c0, y.c1) of the E2' point.
+__global__ void __launch_bounds__(64) k_h2c_sswu(size_t B, const uint8_t* msgs32, const int* status, Fp* U) {
+  const size_t k = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = k >> 1;
+  const int t = (int)(k & 1);
+  if (i >= B) return;
+  if (status && !status[i]) return;
+  Fp2 u[2];
+  hash_to_field_fp2(u, msgs32 + 32 * i, 32, DST_POP_FAV, 43);
+  Fp2 x, y;
+  map_to_curve_sswu(x, y, u[t]);
+  Fp* o = U + 8 * i + 4 * t;
+  o[0] = x.c0;
+  o[1] = x.c1;
+  o[2] = y.c0;
+  o[3] = y.c1;
+}
+
+// (2) isogeny, sum, cofactor clearing and affine conversion on the VM.
+// flag[i] = 1 when an isogeny denominator vanished (the item is recomputed
+// by k_h2c_fallback; unreachable for SHA-256 outputs in practice).
+template <int G>
+__global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, const Fp* U, G2A* H, int* flag) {
+  __shared__ Fp s[WP_NCONST + G * WL_HC_STRIDE];
+  __shared__ int live[G];
+  const int lane = threadIdx.x;
+  const size_t i0 = (size_t)blockIdx.x * G;
+  vm_load_consts(s);
+  if (lane < G) {
+    const size_t i = i0 + lane;
+    live[lane] = i < B && (!status || status[i]);
+  }
+  __syncthreads();
+  const int item0 = WP_NCONST;
+  for (int k = lane; k < 8 * G; k += 64) {
+    const int g = k >> 3, j = k & 7;
+    s[item0 + g * WL_HC_STRIDE + WL_HC_U + j] = live[g] ? U[8 * (i0 + g) + j] : fp_zero();
+  }
+  __syncthreads();
+  vm_run<G>(VM_PROG(HC_ISO), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XQ_0), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XQ_1), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XQ_2), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XQ_3), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XQ_4), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XQ_5), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_PRE), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XA_0), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XA_1), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XA_2), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XA_3), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XA_4), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_XA_5), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_POST), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_NORM), s, item0, WL_HC_STRIDE, nullptr);
+  if (lane < G) {  // 1 / norm(Z): one inversion per item
+    Fp* r = s + item0 + lane * WL_HC_STRIDE;
+    r[WL_HC_NI] = fp_inv(r[WL_HC_N]);
+  }
+  __syncthreads();
+  vm_run<G>(VM_PROG(HC_INVFIN), s, item0, WL_HC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(HC_TOAFF), s, item0, WL_HC_STRIDE, nullptr);
+  if (lane < G) {
+    const size_t i = i0 + lane;
+    if (i < B) {
+      const Fp* r = s + item0 + lane * WL_HC_STRIDE;
+      const bool bad = fp_is_zero(r[WL_HC_IZ]) && fp_is_zero(r[WL_HC_IZ + 1]);
+      const bool bad2 = fp_is_zero(r[WL_HC_IZ + 2]) && fp_is_zero(r[WL_HC_IZ + 3]);
+      const bool inf = fp_is_zero(r[WL_HC_N]);
+      G2A h;
+      h.x = Fp2{r[WL_HC_XY], r[WL_HC_XY + 1]};
+      h.y = Fp2{r[WL_HC_XY + 2], r[WL_HC_XY + 3]};
+      h.inf = inf || !live[lane];
+      if (!live[lane]) {
+        h.x = fp2_zero();
+        h.y = fp2_zero();
+      }
+      H[i] = h;
+      flag[i] = live[lane] && (bad || bad2);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) k_h2c_fallback(size_t B, const uint8_t* msgs32, const int* flag, G2A* H) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || !flag[i]) return;
+  H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_FAV, 43));
+}
+
+// ----------------------------------------------------------- signatures --
+// RLC scalar r_i = first 8 bytes of SHA-256(seed || i || msg || sig), nonzero.
+static __device__ uint64_t rlc_scalar_fav(const uint8_t* seed32, uint64_t i, const uint8_t* msg32,
+                                          const uint8_t* sig96) {
+  Sha256 sh;
+  sha256_init(sh);
+  sha256_update(sh, seed32, 32);
+  for (int k = 0; k < 8; k++) sha256_byte(sh, (uint8_t)(i >> (8 * k)));
+  sha256_update(sh, msg32, 32);
+  sha256_update(sh, sig96, 96);
+  uint8_t d[32];
+  sha256_final(sh, d);
+  uint64_t r = 0;
+  for (int k = 0; k < 8; k++) r = (r << 8) | d[k];
+  return r ? r : 1;
+}
+
+// (1) lane per item: aggregate key to affine, signature decompression (no
+// subgroup check yet), RLC scalar.  The identity signature can only verify
+// against the identity key, which the gather already rejected.
+__global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
+                                                   const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff,
+                                                   G2A* sig, uint64_t* rsc) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B) return;
+  G1A a{fp_zero(), fp_zero(), true};
+  G2A q{fp2_zero(), fp2_zero(), true};
+  int st = status[i];
+  if (st) {
+    a = jac_to_aff(apk[i]);
+    if (a.inf) st = 0;
+  }
+  if (st && g2_decompress(q, sigs96 + 96 * i) != DEC_OK) st = 0;
+  rsc[i] = st ? rlc_scalar_fav(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i) : 0;
+  apk_aff[i] = a;
+  sig[i] = q;
+  status[i] = st;
+}
+
+// (2) the three signature-side chains, 64 steps, then the subgroup verdict,
+// r * apk to affine and r * sigma to Jacobian.
+template <int G>
+__global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G1A* apk_aff, const G2A* sig,
+                                                 const uint64_t* rsc, G1A* rP, G2J* rS) {
+  __shared__ Fp s[WP_NCONST + G * WL_SG_STRIDE];
+  __shared__ int live[G];
+  __shared__ uint32_t pred[G];
+  const int lane = threadIdx.x;
+  const size_t i0 = (size_t)blockIdx.x * G;
+  vm_load_consts(s);
+  uint64_t r = 0;
+  if (lane < G) {
+    const size_t i = i0 + lane;
+    live[lane] = i < B && status[i];
+    r = live[lane] ? rsc[i] : 0;
+  }
+  __syncthreads();
+  const int item0 = WP_NCONST;
+  // sigma (4) | apk (2) | M = (sigma, 1) (6) | R = (0:1:0) (3) | S = (0:1:0) (6)
+  for (int k = lane; k < 21 * G; k += 64) {
+    const int g = k / 21, j = k % 21;
+    const size_t i = i0 + g;
+    Fp v = fp_zero();
+    if (live[g]) {
+      const G2A& q = sig[i];
+      if (j < 4) v = j == 0 ? q.x.c0 : (j == 1 ? q.x.c1 : (j == 2 ? q.y.c0 : q.y.c1));
+      else if (j < 6) v = j == 4 ? apk_aff[i].x : apk_aff[i].y;
+      else if (j < 10) v = j == 6 ? q.x.c0 : (j == 7 ? q.x.c1 : (j == 8 ? q.y.c0 : q.y.c1));
+      else if (j == 10) v = FP_ONE;
+    }
+    if (j == 13 || j == 17) v = FP_ONE;  // Y of R and Re Y of S
+    s[item0 + g * WL_SG_STRIDE + j] = v;
+  }
+  __syncthreads();
+  for (int b = 63; b >= 0; --b) {
+    if (lane < G) pred[lane] = (uint32_t)(r >> b) & 1u;
+    __syncthreads();
+    if (b == 63)
+      vm_run<G>(VM_PROG(SG_STEP0), s, item0, WL_SG_STRIDE, pred);
+    else if ((X_ABS >> b) & 1ull)
+      vm_run<G>(VM_PROG(SG_STEP2), s, item0, WL_SG_STRIDE, pred);
+    else
+      vm_run<G>(VM_PROG(SG_STEP1), s, item0, WL_SG_STRIDE, pred);
+  }
+  vm_run<G>(VM_PROG(SG_SUBCHK), s, item0, WL_SG_STRIDE, nullptr);
+  if (lane < G) {
+    Fp* e = s + item0 + lane * WL_SG_STRIDE;
+    e[WL_SG_NI] = fp_inv(e[WL_SG_R + 2]);
+  }
+  __syncthreads();
+  vm_run<G>(VM_PROG(SG_TOAFF), s, item0, WL_SG_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(SG_TOJAC), s, item0, WL_SG_STRIDE, nullptr);
+  if (lane < G) {
+    const size_t i = i0 + lane;
+    if (i < B) {
+      const Fp* e = s + item0 + lane * WL_SG_STRIDE;
+      bool ok = live[lane];
+      // sigma in G2  <=>  psi(sigma) == -[|x|] sigma  (differences zero, M not the identity)
+      for (int j = 0; j < 4; j++) ok = ok && fp_is_zero(e[WL_SG_D + j]);
+      ok = ok && !(fp_is_zero(e[WL_SG_D + 4]) && fp_is_zero(e[WL_SG_D + 5]));
+      if (ok) {
+        rP[i] = G1A{e[WL_SG_XY1], e[WL_SG_XY1 + 1], false};
+        G2J j;
+        j.x = Fp2{e[WL_SG_SJ], e[WL_SG_SJ + 1]};
+        j.y = Fp2{e[WL_SG_SJ + 2], e[WL_SG_SJ + 3]};
+        j.z = Fp2{e[WL_SG_SJ + 4], e[WL_SG_SJ + 5]};
+        rS[i] = j;
+      } else {
+        rP[i] = G1A{fp_zero(), fp_zero(), true};
+        rS[i] = jac_identity<Fp2>();
+      }
+      status[i] = ok ? 1 : 0;
+    }
+  }
+}
+
+static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, G2A* H, int* flag) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_h2c_sswu, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs32, status, U);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_h2c_vm<FAV_G>, dim3(nblk(B, FAV_G)), dim3(64), 0, st, B, status, U, H, flag);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_h2c_fallback, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, flag, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
+                             const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff, G2A* sig,
+                             uint64_t* rsc) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_decode, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, sigs96, seed32, apk, status,
+                     apk_aff, sig, rsc);
+  return hipGetLastError();
+}
+
+hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const G1A* apk_aff, const G2A* sig,
+                         const uint64_t* rsc, G1A* rP, G2J* rS) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_vm<FAV_G>, dim3(nblk(B, FAV_G)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP, rS);
+  return hipGetLastError();
+}
+
+}  // namespace bls

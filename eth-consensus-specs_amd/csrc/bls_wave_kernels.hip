@@ -35,7 +35,7 @@ constexpr int imax(int a, int b) { return a > b ? a : b; }
 constexpr int ML_G = 2;  // pairs per workgroup
 
 template <int G>
-__global__ void __launch_bounds__(64) k_miller_vm(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* fout) {
+__global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* fout) {
   __shared__ Fp slots[WP_NCONST + G * WL_ML_STRIDE];
   __shared__ int skip[G];
   const int lane = threadIdx.x;

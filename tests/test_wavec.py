@@ -221,7 +221,7 @@ def test_iso_and_cofactor_programs_match_hash_to_g2():
     u0, u1 = O.hash_to_field_fp2(msg, 2, O.DST_POP)
     p0, p1 = O.map_to_curve_sswu(u0), O.map_to_curve_sswu(u1)
     frame0 = [p0[0][0], p0[0][1], p0[1][0], p0[1][1], p1[0][0], p1[0][1], p1[1][0], p1[1][1]]
-    q = run(PROGS["ISO_PAIR"], [frame0, [0] * 6])[1]
+    q = run(PROGS["ISO_PAIR"], [frame0, [0] * 6, [0] * 4])[1]
     assert g2_aff(q) == O.g2_add(O.iso_map(p0), O.iso_map(p1))
 
     def xmul(v):
@@ -248,3 +248,25 @@ def test_g1_to_affine_program():
     v = g1_proj(p)
     xy = run(PROGS["G1_TOAFF"], [v, [pow(v[2], -1, O.P)], [0, 0]])[2]
     assert tuple(xy) == p
+
+
+def test_signature_step_programs():
+    """64 steps of SIG_STEP{0,1,2}: M = [|x|] sigma, R = r apk, S = r sigma."""
+    sig = O.g2_mul(O.G2_GEN, 0x1234_5678_9ABC)
+    apk = O.g1_mul(O.G1_GEN, 0xDEADBEEF)
+    r = rng.getrandbits(64) | (1 << 63)
+    fr = [[sig[0][0], sig[0][1], sig[1][0], sig[1][1]], [apk[0], apk[1]],
+          [sig[0][0], sig[0][1], sig[1][0], sig[1][1], 1, 0], g1_proj(None), g2_proj(None)]
+    for b in range(63, -1, -1):
+        mode = 0 if b == 63 else (2 if (O.X_ABS >> b) & 1 else 1)
+        fr = run(PROGS[f"SIG_STEP{mode}"], fr, pred=(r >> b) & 1)[:5]
+    assert g2_aff(fr[2]) == O.g2_mul(sig, O.X_ABS)
+    assert g1_aff(fr[3]) == O.g1_mul(apk, r)
+    assert g2_aff(fr[4]) == O.g2_mul(sig, r)
+    out = run(PROGS["G2_SUBCHK"], [fr[0], fr[2], [0] * 6])[2]
+    assert out[:4] == [0, 0, 0, 0] and out[4:6] != [0, 0]
+    jac = run(PROGS["G2_PROJ2JAC"], [fr[4], [0] * 6])[1]
+    z = (jac[4], jac[5])
+    zi = O.f2_inv(z)
+    zi2 = O.f2_mul(zi, zi)
+    assert (O.f2_mul((jac[0], jac[1]), zi2), O.f2_mul((jac[2], jac[3]), O.f2_mul(zi2, zi))) == O.g2_mul(sig, r)

@@ -688,7 +688,8 @@ def prog_iso_pair(c):
         xnum, xden, ynum, yden = poly(ISO_XNUM), poly(ISO_XDEN), poly(ISO_YNUM), poly(ISO_YDEN)
         # (xnum/xden, y ynum/yden) -> projective (xnum yden : y ynum xden : xden yden)
         pts.append((xnum * yden, (y * ynum) * xden, xden * yden))
-    return {1: pt_out(rcb_add(pts[0], pts[1], B2_3))}
+    z0, z1 = pts[0][2], pts[1][2]
+    return {1: pt_out(rcb_add(pts[0], pts[1], B2_3)), 2: [z0.a, z0.b, z1.a, z1.b]}
 
 
 def prog_clear_pre(c):
@@ -739,6 +740,43 @@ def prog_fp2_inv_finish(c):
     return {2: [a.a * n, -(a.b * n)]}
 
 
+def make_sig_step(mode):
+    """One bit step of the three signature-side chains of an FAV item:
+      frame 0: sigma affine (x, y)          frame 1: apk affine (x, y)
+      frame 2: M (projective, [|x|] sigma chain)
+      frame 3: R (G1 projective, r * apk)   frame 4: S (G2 projective, r * sigma)
+    R <- pred ? 2R + apk : 2R and S <- pred ? 2S + sigma : 2S (pred = bit of
+    the item's RLC scalar); M <- 2M (mode 1), 2M + sigma (mode 2), unchanged
+    (mode 0, the leading bit)."""
+
+    def prog(c):
+        sig = (f2_from_frame(c, 0, 0), f2_from_frame(c, 0, 2))
+        apk = (inp(c, 1, 0), inp(c, 1, 1))
+        out = {}
+        if mode:
+            M = rcb_dbl(pt_from_frame(c, 2, 0, True), B2_3)
+            if mode == 2:
+                M = rcb_add_aff(M, sig, B2_3)
+            out[2] = pt_out(M)
+        R = pt_from_frame(c, 3, 0, False)
+        D = rcb_dbl(R, B1_3)
+        A = rcb_add_aff(D, apk, B1_3)
+        out[3] = [sel(c, a, d) for a, d in zip(pt_out(A), pt_out(D))]
+        S = pt_from_frame(c, 4, 0, True)
+        D2 = rcb_dbl(S, B2_3)
+        A2 = rcb_add_aff(D2, sig, B2_3)
+        out[4] = [sel(c, a, d) for a, d in zip(pt_out(A2), pt_out(D2))]
+        return out
+
+    return prog
+
+
+def prog_g2_proj_to_jac(c):
+    """frame 0: (X : Y : Z) homogeneous; out frame 1: Jacobian (X Z, Y Z^2, Z)."""
+    X, Y, Z = pt_from_frame(c, 0, 0, True)
+    return {1: pt_out((X * Z, Y * Z.sqr(), Z))}
+
+
 X_RUNS = xabs_runs()
 
 PROGRAMS = {
@@ -755,13 +793,17 @@ PROGRAMS = {
     "G1_DAS": (make_dbl_add_sel(False), [3, 2]),
     "G2_DAS": (make_dbl_add_sel(True), [6, 4]),
     "G2_SUBCHK": (prog_g2_aff_to_proj_psi_check, [4, 6, 6]),
-    "ISO_PAIR": (prog_iso_pair, [8, 6]),
+    "ISO_PAIR": (prog_iso_pair, [8, 6, 4]),
     "CLEAR_PRE": (prog_clear_pre, [6, 6, 6, 6]),
     "CLEAR_POST": (prog_clear_post, [6, 6, 6]),
     "G2_TOAFF": (prog_proj_to_aff2, [6, 2, 4]),
     "G1_TOAFF": (prog_proj_to_aff1, [3, 1, 2]),
     "FP2_NORM": (prog_fp2_norm, [2, 1]),
     "FP2_INVFIN": (prog_fp2_inv_finish, [2, 1, 2]),
+    "SIG_STEP0": (make_sig_step(0), [4, 2, 6, 3, 6]),
+    "SIG_STEP1": (make_sig_step(1), [4, 2, 6, 3, 6]),
+    "SIG_STEP2": (make_sig_step(2), [4, 2, 6, 3, 6]),
+    "G2_PROJ2JAC": (prog_g2_proj_to_jac, [6, 6]),
 }
 for _k, _add in X_RUNS:
     # the output frame may alias the running value (in-place runs)
@@ -1089,6 +1131,31 @@ def define_instances(progs):
         cur = R(2) if i == 0 else R(1)
         instance(f"FE_POWX_{i}", nm, [cur, R(2), R(1)], 84)
     instance("FE_CUBE", "CYC_1M", [R(0), R(0), R(5)], 84)
+    # hash_to_G2 tail: SSWU points | Q | M | A | C | H | izs | Z (norm in) | N | NI | ZI | XY | scratch
+    H = dict(U=0, Q=8, M=14, A=20, C=26, H=32, IZ=38, N=42, NI=43, ZI=44, XY=46, S=50)
+    hs = max(sc["ISO_PAIR"], sc["CLEAR_PRE"], sc["CLEAR_POST"], sc["FP2_NORM"], sc["FP2_INVFIN"],
+             sc["G2_TOAFF"], *[sc[n] for n in sc if n.startswith("G2X_")])
+    layout("HC", STRIDE=H["S"] + hs, **H)
+    instance("HC_ISO", "ISO_PAIR", [H["U"], H["Q"], H["IZ"]], H["S"])
+    for i, (k, add) in enumerate(X_RUNS):  # M = [|x|] Q  and later  M = [|x|] A
+        nm = f"G2X_{k}{'A' if add else ''}"
+        instance(f"HC_XQ_{i}", nm, [H["Q"] if i == 0 else H["M"], H["Q"], H["M"]], H["S"])
+        instance(f"HC_XA_{i}", nm, [H["A"] if i == 0 else H["M"], H["A"], H["M"]], H["S"])
+    instance("HC_PRE", "CLEAR_PRE", [H["Q"], H["M"], H["A"], H["C"]], H["S"])
+    instance("HC_POST", "CLEAR_POST", [H["C"], H["M"], H["H"]], H["S"])
+    instance("HC_NORM", "FP2_NORM", [H["H"] + 4, H["N"]], H["S"])
+    instance("HC_INVFIN", "FP2_INVFIN", [H["H"] + 4, H["NI"], H["ZI"]], H["S"])
+    instance("HC_TOAFF", "G2_TOAFF", [H["H"], H["ZI"], H["XY"]], H["S"])
+    # signature side: sigma | apk | M | R | S | D (subgroup check) | N | NI | XY1 | SJ | scratch
+    G = dict(SIG=0, APK=4, M=6, R=12, S=15, D=21, N=27, NI=28, XY1=29, SJ=31, SC=37)
+    gs = max(sc["SIG_STEP0"], sc["SIG_STEP1"], sc["SIG_STEP2"], sc["G2_SUBCHK"], sc["G1_TOAFF"],
+             sc["G2_PROJ2JAC"])
+    layout("SG", STRIDE=G["SC"] + gs, **G)
+    for m in range(3):
+        instance(f"SG_STEP{m}", f"SIG_STEP{m}", [G["SIG"], G["APK"], G["M"], G["R"], G["S"]], G["SC"])
+    instance("SG_SUBCHK", "G2_SUBCHK", [G["SIG"], G["M"], G["D"]], G["SC"])
+    instance("SG_TOAFF", "G1_TOAFF", [G["R"], G["NI"], G["XY1"]], G["SC"])
+    instance("SG_TOJAC", "G2_PROJ2JAC", [G["S"], G["SJ"]], G["SC"])
 
 
 def compile_all():
