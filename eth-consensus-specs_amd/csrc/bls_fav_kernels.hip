@@ -8,6 +8,7 @@
 //     r * apk in G1, r * sigma in G2) advanced together one scalar bit per
 //     step with complete (exception-free) projective formulas.
 #include "bls_kernels.h"
+#include "bls_lane.h"
 #include "bls_vm.h"
 
 namespace bls {
@@ -30,7 +31,7 @@ __global__ void __launch_bounds__(64) k_h2c_sswu(size_t B, const uint8_t* msgs32
   Fp2 u[2];
   hash_to_field_fp2(u, msgs32 + 32 * i, 32, DST_POP_FAV, 43);
   Fp2 x, y;
-  map_to_curve_sswu(x, y, u[t]);
+  map_to_curve_sswu_lane(x, y, u[t]);
   Fp* o = U + 8 * i + 4 * t;
   o[0] = x.c0;
   o[1] = x.c1;
@@ -141,7 +142,7 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
     a = jac_to_aff(apk[i]);
     if (a.inf) st = 0;
   }
-  if (st && g2_decompress(q, sigs96 + 96 * i) != DEC_OK) st = 0;
+  if (st && g2_decompress_lane(q, sigs96 + 96 * i) != DEC_OK) st = 0;
   rsc[i] = st ? rlc_scalar_fav(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i) : 0;
   apk_aff[i] = a;
   sig[i] = q;

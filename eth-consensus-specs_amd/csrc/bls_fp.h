@@ -159,9 +159,17 @@ BLS_HDNI Fp fp_mul(const Fp& a, const Fp& b) {
   return fp_mul_digits(x, y);
 }
 
+// Inline product (hot loops that keep operands in registers).
+BLS_HD Fp fp_mul_i(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14];
+  fp_unpack29(x, a);
+  fp_unpack29(y, b);
+  return fp_mul_digits(x, y);
+}
+
 // Squaring: off-diagonal digit products once, doubled (105 + 14 instead of
 // 196 products for the a*a half).
-BLS_HDNI Fp fp_sqr(const Fp& a) {
+BLS_HD Fp fp_sqr_i(const Fp& a) {
   uint32_t x[14], m[14], r[14];
   fp_unpack29(x, a);
   uint64_t acc = 0;
@@ -191,6 +199,8 @@ BLS_HDNI Fp fp_sqr(const Fp& a) {
   r[13] = (uint32_t)acc;
   return fp_reduce_once(fp_pack29(r));
 }
+
+BLS_HDNI Fp fp_sqr(const Fp& a) { return fp_sqr_i(a); }
 
 // a^e for a fixed exponent given as 12 limbs with known bit length.
 BLS_HDNI Fp fp_pow(const Fp& a, const uint32_t* e, int nbits) {

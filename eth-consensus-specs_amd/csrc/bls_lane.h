@@ -1,0 +1,156 @@
+// Per-lane arithmetic for the long sequential chains of the FAV batch (one
+// lane owns one value; no cross-lane traffic):
+//   - fp_pow_w3: fixed-exponent sliding-window (w = 3) exponentiation with the
+//     multiplications inlined in one loop body, so the 379-bit square-root
+//     exponents cost ~379 squarings + ~95 products with operands in VGPRs;
+//   - fp2_sqrt_lane: square root in Fp2 with two Fp exponentiations and no
+//     inversion or Jacobi symbol (see below);
+//   - map_to_curve_sswu_lane: RFC 9380 simplified SWU whose second square
+//     root needs only one exponentiation (its norm root is derived);
+//   - g2_decompress_lane: ZCash signature decoding with fp2_sqrt_lane.
+// Results are identical to bls_h2c.h / bls_curve.h (the same canonical
+// points; tests/hostcheck compares both with the oracle).
+#pragma once
+#include "bls_curve.h"
+#include "bls_sha256.h"
+
+namespace bls {
+
+// a^e, e given as little-endian u32 limbs with bit nbits-1 set.  Control
+// flow depends only on e (uniform across lanes).
+BLS_HD Fp fp_pow_w3(const Fp& a, const uint32_t* e, int nbits) {
+  const Fp a2 = fp_sqr_i(a);
+  const Fp t1 = a;
+  const Fp t3 = fp_mul_i(t1, a2);
+  const Fp t5 = fp_mul_i(t3, a2);
+  const Fp t7 = fp_mul_i(t5, a2);
+  Fp r = t1;
+  bool started = false;
+  int i = nbits - 1;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      r = fp_sqr_i(r);
+      --i;
+      continue;
+    }
+    int j = i - 2 < 0 ? 0 : i - 2;  // window [i .. j], ending on a set bit
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) ++j;
+    uint32_t w = 0;
+    for (int k = i; k >= j; --k) w = (w << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
+    const Fp& m = w == 1u ? t1 : (w == 3u ? t3 : (w == 5u ? t5 : t7));
+    if (!started) {
+      r = m;
+      started = true;
+    } else {
+      for (int k = i; k >= j; --k) r = fp_sqr_i(r);
+      r = fp_mul_i(r, m);
+    }
+    i = j - 1;
+  }
+  return r;
+}
+
+BLS_HD Fp fp_sqrt_cand(const Fp& a) { return fp_pow_w3(a, EXP_SQRT, EXP_SQRT_BITS); }      // a^((p+1)/4)
+BLS_HD Fp fp_pow_pm3_4(const Fp& a) { return fp_pow_w3(a, EXP_SQRT_M3, EXP_SQRT_M3_BITS); }  // a^((p-3)/4)
+
+// Square root of a = a0 + a1 i with a1 != 0, given n with n^2 = a0^2 + a1^2.
+// t = (a0 + n)/2 and s = t^((p-3)/4):
+//   t a square:      x0 = t s,        x1 = a1 s / 2     (x0 = sqrt t, 1/x0 = s)
+//   t a non-square:  x0 = a1 s / 2,   x1 = -t s         (p = 3 mod 8 makes
+//                    s^2 = -1/t, i.e. s = sqrt(-1/t), and x0^2 - x1^2 = a0)
+// Both cases satisfy (x0 + x1 i)^2 = a; the caller picks the sign.
+BLS_HD Fp2 fp2_sqrt_from_norm_root(const Fp2& a, const Fp& n) {
+  const Fp t = fp_mul_i(fp_add(a.c0, n), FP_INV2);
+  const Fp s = fp_pow_pm3_4(t);
+  const Fp ts = fp_mul_i(t, s);
+  const Fp hs = fp_mul_i(fp_mul_i(a.c1, FP_INV2), s);
+  if (fp_is_one(fp_mul_i(ts, s))) return Fp2{ts, hs};
+  return Fp2{hs, fp_neg(ts)};
+}
+
+// Some square root of a; false if a is not a square in Fp2.
+BLS_HDNI bool fp2_sqrt_lane(Fp2& out, const Fp2& a) {
+  if (fp_is_zero(a.c1)) {  // a in Fp: s = a0^((p+1)/4), s^2 = a0 or -a0
+    const Fp s = fp_sqrt_cand(a.c0);
+    out = fp_eq(fp_sqr_i(s), a.c0) ? Fp2{s, fp_zero()} : Fp2{fp_zero(), s};
+    return true;  // every element of Fp is a square in Fp2
+  }
+  const Fp nrm = fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1));
+  const Fp n = fp_sqrt_cand(nrm);
+  if (!fp_eq(fp_sqr_i(n), nrm)) return false;
+  out = fp2_sqrt_from_norm_root(a, n);
+  return true;
+}
+
+BLS_HD int fp2_sgn0_lane(const Fp2& a_mont) {
+  const Fp a0 = fp_from_mont(a_mont.c0), a1 = fp_from_mont(a_mont.c1);
+  return (int)(a0.l[0] & 1u) | ((int)fp_is_zero(a0) & (int)(a1.l[0] & 1u));
+}
+
+// RFC 9380 simplified SWU on E2' -> affine (x, y).  If g(x1) is not a square,
+// g(x2) = Z^3 u^6 g(x1) and c = norm(g(x1))^((p+1)/4) satisfies
+// c^2 = -norm(g(x1)), so norm(g(x2)) has the root K c norm(u)^3 with
+// K = sqrt(-norm(Z)^3) (SSWU_K_NORM): one exponentiation saved.
+BLS_HDNI void map_to_curve_sswu_lane(Fp2& x, Fp2& y, const Fp2& u) {
+  const Fp2 u2 = fp2_sqr(u);
+  const Fp2 zu2 = fp2_mul(SSWU_Z, u2);
+  const Fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+  const Fp2 x1 = fp2_is_zero(den) ? SSWU_B_OVER_ZA : fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv(den)));
+  const Fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
+  const Fp nrm1 = fp_add(fp_sqr_i(gx1.c0), fp_sqr_i(gx1.c1));
+  const Fp c = fp_sqrt_cand(nrm1);
+  Fp2 gx;
+  Fp n;
+  if (fp_eq(fp_sqr_i(c), nrm1)) {
+    x = x1;
+    gx = gx1;
+    n = c;
+  } else {
+    x = fp2_mul(zu2, x1);
+    gx = fp2_add(fp2_mul(fp2_add(fp2_sqr(x), SSWU_A), x), SSWU_B);
+    const Fp nu = fp_add(fp_sqr_i(u.c0), fp_sqr_i(u.c1));
+    n = fp_mul_i(fp_mul_i(SSWU_K_NORM, c), fp_mul_i(fp_sqr_i(nu), nu));
+  }
+  Fp2 yy;
+  if (fp_is_zero(gx.c1)) {
+    fp2_sqrt_lane(yy, gx);
+  } else {
+    yy = fp2_sqrt_from_norm_root(gx, n);
+  }
+  if (fp2_sgn0_lane(u) != fp2_sgn0_lane(yy)) yy = fp2_neg(yy);
+  y = yy;
+}
+
+// 96 bytes (x.c1 || x.c0) -> affine G2 (py_ecc signature_to_G2 rules); no
+// subgroup check.
+BLS_HDNI int g2_decompress_lane(G2A& out, const uint8_t* b) {
+  const uint8_t f = b[0];
+  const bool c_flag = f & 0x80, b_flag = f & 0x40, a_flag = f & 0x20;
+  out.inf = false;
+  if (!c_flag) return DEC_BAD_FLAGS;
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; i++) tmp[i] = b[i];
+  tmp[0] &= 0x1f;
+  const Fp x1 = raw_from_be48(tmp);
+  const Fp x0 = raw_from_be48(b + 48);
+  const bool x_zero = fp_is_zero(x1) && fp_is_zero(x0);
+  if (b_flag != x_zero) return DEC_BAD_FLAGS;
+  if (x_zero) {
+    if (a_flag) return DEC_BAD_FLAGS;
+    out.inf = true;
+    out.x = fp2_zero();
+    out.y = fp2_zero();
+    return DEC_INFINITY;
+  }
+  if (!raw_lt_p(x1) || !raw_lt_p(x0)) return DEC_NOT_FIELD;
+  const Fp2 xm{fp_to_mont(x0), fp_to_mont(x1)};
+  const Fp2 rhs = fp2_add(fp2_mul(fp2_sqr(xm), xm), FP2_B2);
+  Fp2 y;
+  if (!fp2_sqrt_lane(y, rhs)) return DEC_NOT_ON_CURVE;
+  if (fp2_lex_largest(y) != a_flag) y = fp2_neg(y);
+  out.x = xm;
+  out.y = y;
+  return DEC_OK;
+}
+
+}  // namespace bls

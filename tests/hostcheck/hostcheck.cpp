@@ -4,6 +4,7 @@
 // by the product shim.  All values cross the boundary as canonical
 // big-endian integers (48 bytes per Fp).
 #include "bls_ops.h"
+#include "bls_lane.h"
 #include <string.h>
 using namespace bls;
 
@@ -89,3 +90,14 @@ void hc_g1_mul_u256(const uint8_t* p, const uint32_t* k, uint8_t* o48) {
 }
 extern "C" int hc_fp_is_square(const uint8_t* a) { return fp_is_square(in_fp(a)); }
 extern "C" void hc_fp_sqr(const uint8_t* a, uint8_t* o) { out_fp(o, fp_sqr(in_fp(a))); }
+// per-lane chain math (bls_lane.h)
+extern "C" int hc_fp2_sqrt_lane(const uint8_t* a, uint8_t* o) { Fp2 r; int ok = fp2_sqrt_lane(r, in_fp2(a)); out_fp2(o, r); return ok; }
+extern "C" void hc_map_to_curve_lane(const uint8_t* u, uint8_t* o) {
+  Fp2 x, y; map_to_curve_sswu_lane(x, y, in_fp2(u)); out_fp2(o, x); out_fp2(o + 96, y);
+}
+extern "C" int hc_g2_decompress_lane(const uint8_t* b, uint8_t* o) {
+  G2A a; int st = g2_decompress_lane(a, b);
+  if (st == DEC_OK) { out_fp2(o, a.x); out_fp2(o + 96, a.y); }
+  return st;
+}
+extern "C" void hc_fp_pow_w3(const uint8_t* a, const uint32_t* e, int nbits, uint8_t* o) { out_fp(o, fp_pow_w3(in_fp(a), e, nbits)); }

@@ -195,3 +195,32 @@ def test_jacobi_and_sqr():
         assert H.b_fp(H.call("hc_fp_sqr", H.fp_b(a), out=48)) == a * a % O.P
     for a in (0, 1, O.P - 1, 4, 2):
         assert H.call("hc_fp_is_square", H.fp_b(a)) == (1 if O.fp_is_square(a) else 0)
+
+
+def test_lane_chain_math():
+    import ctypes
+    for e in (3, 5, 0x7, 0xB1, (O.P + 1) // 4, (O.P - 3) // 4, (1 << 200) + 12345):
+        a = rfp()
+        limbs = (ctypes.c_uint32 * 12)(*[(e >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+        got = H.b_fp(H.call("hc_fp_pow_w3", H.fp_b(a), limbs, e.bit_length(), out=48))
+        assert got == pow(a, e, O.P)
+    # Fp2 square roots: random squares, pure-real / pure-imaginary, non-squares
+    cases = [O.f2_sqr(rfp2()) for _ in range(20)] + [(5, 0), (O.P - 5, 0), (0, 7), (0, 0), (rfp(), 0)]
+    for a in cases:
+        ok, r = H.call("hc_fp2_sqrt_lane", H.fp2_b(a), out=96, ret=True)
+        assert ok == 1 and O.f2_sqr(H.b_fp2(r)) == a
+    ns = [x for x in (rfp2() for _ in range(40)) if not O.f2_is_square(x)][:5]
+    for a in ns:
+        ok, _ = H.call("hc_fp2_sqrt_lane", H.fp2_b(a), out=96, ret=True)
+        assert ok == 0
+    # SSWU: both branches (g(x1) square or not) over random inputs
+    for _ in range(12):
+        u = rfp2()
+        out = H.call("hc_map_to_curve_lane", H.fp2_b(u), out=192)
+        assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
+    # decompression incl. both y signs
+    for k in (1, 2, 3, 0xDEADBEEF, 0x5EED5EED):
+        q = O.g2_mul(O.G2_GEN, k)
+        for pt in (q, O.g2_neg(q)):
+            st, out = H.call("hc_g2_decompress_lane", O.g2_compress(pt), out=192, ret=True)
+            assert st == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == pt
