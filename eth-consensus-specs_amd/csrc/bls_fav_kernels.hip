@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(64) k_h2c_sswu(size_t B, const uint8_t* msgs32
 // by k_h2c_fallback; unreachable for SHA-256 outputs in practice).
 template <int G>
 __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, const Fp* U, G2A* H, int* flag) {
-  __shared__ Fp s[WP_NCONST + G * WL_HC_STRIDE];
+  __shared__ Fd s[WP_NCONST + G * WL_HC_STRIDE];
   __shared__ int live[G];
   const int lane = threadIdx.x;
   const size_t i0 = (size_t)blockIdx.x * G;
@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, c
   const int item0 = WP_NCONST;
   for (int k = lane; k < 8 * G; k += 64) {
     const int g = k >> 3, j = k & 7;
-    s[item0 + g * WL_HC_STRIDE + WL_HC_U + j] = live[g] ? U[8 * (i0 + g) + j] : fp_zero();
+    s[item0 + g * WL_HC_STRIDE + WL_HC_U + j] = live[g] ? fd_from_fp(U[8 * (i0 + g) + j]) : fd_zero();
   }
   __syncthreads();
   vm_run<G>(VM_PROG(HC_ISO), s, item0, WL_HC_STRIDE, nullptr);
@@ -77,8 +77,8 @@ __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, c
   vm_run<G>(VM_PROG(HC_POST), s, item0, WL_HC_STRIDE, nullptr);
   vm_run<G>(VM_PROG(HC_NORM), s, item0, WL_HC_STRIDE, nullptr);
   if (lane < G) {  // 1 / norm(Z): one inversion per item
-    Fp* r = s + item0 + lane * WL_HC_STRIDE;
-    r[WL_HC_NI] = fp_inv(r[WL_HC_N]);
+    Fd* r = s + item0 + lane * WL_HC_STRIDE;
+    r[WL_HC_NI] = fd_from_fp(fp_inv(fp_from_fd(r[WL_HC_N])));
   }
   __syncthreads();
   vm_run<G>(VM_PROG(HC_INVFIN), s, item0, WL_HC_STRIDE, nullptr);
@@ -86,13 +86,13 @@ __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, c
   if (lane < G) {
     const size_t i = i0 + lane;
     if (i < B) {
-      const Fp* r = s + item0 + lane * WL_HC_STRIDE;
-      const bool bad = fp_is_zero(r[WL_HC_IZ]) && fp_is_zero(r[WL_HC_IZ + 1]);
-      const bool bad2 = fp_is_zero(r[WL_HC_IZ + 2]) && fp_is_zero(r[WL_HC_IZ + 3]);
-      const bool inf = fp_is_zero(r[WL_HC_N]);
+      const Fd* r = s + item0 + lane * WL_HC_STRIDE;
+      const bool bad = fd_is_zero(r[WL_HC_IZ]) && fd_is_zero(r[WL_HC_IZ + 1]);
+      const bool bad2 = fd_is_zero(r[WL_HC_IZ + 2]) && fd_is_zero(r[WL_HC_IZ + 3]);
+      const bool inf = fd_is_zero(r[WL_HC_N]);
       G2A h;
-      h.x = Fp2{r[WL_HC_XY], r[WL_HC_XY + 1]};
-      h.y = Fp2{r[WL_HC_XY + 2], r[WL_HC_XY + 3]};
+      h.x = Fp2{fp_from_fd(r[WL_HC_XY]), fp_from_fd(r[WL_HC_XY + 1])};
+      h.y = Fp2{fp_from_fd(r[WL_HC_XY + 2]), fp_from_fd(r[WL_HC_XY + 3])};
       h.inf = inf || !live[lane];
       if (!live[lane]) {
         h.x = fp2_zero();
@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
 template <int G>
 __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G1A* apk_aff, const G2A* sig,
                                                  const uint64_t* rsc, G1A* rP, G2J* rS) {
-  __shared__ Fp s[WP_NCONST + G * WL_SG_STRIDE];
+  __shared__ Fd s[WP_NCONST + G * WL_SG_STRIDE];
   __shared__ int live[G];
   __shared__ uint32_t pred[G];
   const int lane = threadIdx.x;
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
       else if (j == 10) v = FP_ONE;
     }
     if (j == 13 || j == 17) v = FP_ONE;  // Y of R and Re Y of S
-    s[item0 + g * WL_SG_STRIDE + j] = v;
+    s[item0 + g * WL_SG_STRIDE + j] = fd_from_fp(v);
   }
   __syncthreads();
   for (int b = 63; b >= 0; --b) {
@@ -196,8 +196,8 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
   }
   vm_run<G>(VM_PROG(SG_SUBCHK), s, item0, WL_SG_STRIDE, nullptr);
   if (lane < G) {
-    Fp* e = s + item0 + lane * WL_SG_STRIDE;
-    e[WL_SG_NI] = fp_inv(e[WL_SG_R + 2]);
+    Fd* e = s + item0 + lane * WL_SG_STRIDE;
+    e[WL_SG_NI] = fd_from_fp(fp_inv(fp_from_fd(e[WL_SG_R + 2])));
   }
   __syncthreads();
   vm_run<G>(VM_PROG(SG_TOAFF), s, item0, WL_SG_STRIDE, nullptr);
@@ -205,17 +205,17 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
   if (lane < G) {
     const size_t i = i0 + lane;
     if (i < B) {
-      const Fp* e = s + item0 + lane * WL_SG_STRIDE;
+      const Fd* e = s + item0 + lane * WL_SG_STRIDE;
       bool ok = live[lane];
       // sigma in G2  <=>  psi(sigma) == -[|x|] sigma  (differences zero, M not the identity)
-      for (int j = 0; j < 4; j++) ok = ok && fp_is_zero(e[WL_SG_D + j]);
-      ok = ok && !(fp_is_zero(e[WL_SG_D + 4]) && fp_is_zero(e[WL_SG_D + 5]));
+      for (int j = 0; j < 4; j++) ok = ok && fd_is_zero(e[WL_SG_D + j]);
+      ok = ok && !(fd_is_zero(e[WL_SG_D + 4]) && fd_is_zero(e[WL_SG_D + 5]));
       if (ok) {
-        rP[i] = G1A{e[WL_SG_XY1], e[WL_SG_XY1 + 1], false};
+        rP[i] = G1A{fp_from_fd(e[WL_SG_XY1]), fp_from_fd(e[WL_SG_XY1 + 1]), false};
         G2J j;
-        j.x = Fp2{e[WL_SG_SJ], e[WL_SG_SJ + 1]};
-        j.y = Fp2{e[WL_SG_SJ + 2], e[WL_SG_SJ + 3]};
-        j.z = Fp2{e[WL_SG_SJ + 4], e[WL_SG_SJ + 5]};
+        j.x = Fp2{fp_from_fd(e[WL_SG_SJ]), fp_from_fd(e[WL_SG_SJ + 1])};
+        j.y = Fp2{fp_from_fd(e[WL_SG_SJ + 2]), fp_from_fd(e[WL_SG_SJ + 3])};
+        j.z = Fp2{fp_from_fd(e[WL_SG_SJ + 4]), fp_from_fd(e[WL_SG_SJ + 5])};
         rS[i] = j;
       } else {
         rP[i] = G1A{fp_zero(), fp_zero(), true};

@@ -124,8 +124,9 @@ BLS_HD void fp_unpack29_wide(uint32_t d[14], const uint32_t* a) {
 // and one conditional subtraction makes it canonical.  Any operands below
 // 2^390 qualify (x*y/R < 2^374 < p), which lets wave programs feed unreduced
 // linear combinations straight in (bls_wave.h).
-BLS_HD Fp fp_mul_digits(const uint32_t x[14], const uint32_t y[14]) {
-  uint32_t m[14], r[14];
+// Raw form: r = x*y/R as 14 digits with r < 2p (not reduced).
+BLS_HD void fp_mul_digits_raw(uint32_t r[14], const uint32_t x[14], const uint32_t y[14]) {
+  uint32_t m[14];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 27; k++) {
@@ -148,6 +149,11 @@ BLS_HD Fp fp_mul_digits(const uint32_t x[14], const uint32_t y[14]) {
     acc >>= 29;
   }
   r[13] = (uint32_t)acc;  // result < 2p < 2^382
+}
+
+BLS_HD Fp fp_mul_digits(const uint32_t x[14], const uint32_t y[14]) {
+  uint32_t r[14];
+  fp_mul_digits_raw(r, x, y);
   return fp_reduce_once(fp_pack29(r));
 }
 

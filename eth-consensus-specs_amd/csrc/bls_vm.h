@@ -1,19 +1,23 @@
 // Wave-program interpreter (tables from tools/wavec.py, bls_waveprog.h).
 //
 // One 64-lane workgroup runs a program for G items at once.  Every Fp value
-// lives in an LDS slot (48 B).  LDS layout of a workgroup:
-//   slots[0 .. WP_NCONST)              constant pool, loaded once
-//   slots[item0 + g*stride + ix]        slot ix of item g's region (the
-//                                       region layouts WL_* come from wavec)
+// lives in an LDS slot as 14 radix-2^29 digits (Fd, 64 B, canonical residue
+// in Montgomery form R = 2^406) -- the operand format of the product, so no
+// unpacking happens on the hot path.  LDS layout of a workgroup:
+//   slots[0 .. WP_NCONST)          constant pool, loaded once
+//   slots[item0 + g*stride + ix]   slot ix of item g's region (the region
+//                                  layouts WL_* come from wavec)
 // A program level is a set of independent ops; work index k of a level maps
 // to (op j = k / G, item g = k % G), so the G lanes of one op read the same
-// table words and take the same branch.  Levels are separated by a barrier.
+// table words.  Levels are separated by a barrier.
 //
-// Linear combinations are accumulated lazily in a 13-limb (416-bit) running
-// sum that starts at OFF = 256 p: every term costs one add/sub carry chain
-// and no modular reduction (wavec bounds the coefficient mass per form so the
-// sum stays in [0, 2^390)); fp_mul_digits accepts such operands directly and
-// only values stored by lin/sel ops are reduced (vm_reduce).
+// A linear combination sum c_t x_t is accumulated per digit in signed 64-bit
+// lanes: one v_mad_i64_i32 per digit and term, whatever the sign or size of
+// the coefficient (no branches, no carry chains).  The accumulators start at
+// 256 p (wavec bounds the negative coefficient mass by 190 and the positive
+// one so the total stays in [0, 2^390)) written with large digits, so every
+// digit stays non-negative and one parallel carry step turns them into
+// product operands.
 #pragma once
 #include "bls_tower.h"
 #include "bls_waveprog.h"
@@ -22,6 +26,31 @@ namespace bls {
 
 constexpr int VM_MAXT = 12;  // wavec MAX_TERMS
 constexpr int VM_NT = 64;    // lanes per workgroup
+
+struct alignas(16) Fd {
+  uint32_t d[16];  // d[0..13]: radix-2^29 digits; d[14..15] = 0
+};
+
+BLS_HD Fd fd_from_fp(const Fp& a) {
+  Fd r;
+  fp_unpack29(r.d, a);
+  r.d[14] = 0;
+  r.d[15] = 0;
+  return r;
+}
+BLS_HD Fp fp_from_fd(const Fd& a) { return fp_pack29(a.d); }
+BLS_HD bool fd_is_zero(const Fd& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) o |= a.d[i];
+  return o == 0;
+}
+BLS_HD Fd fd_zero() {
+  Fd r;
+#pragma unroll
+  for (int i = 0; i < 16; i++) r.d[i] = 0;
+  return r;
+}
 
 struct VmProg {
   const uint32_t* terms;
@@ -40,80 +69,122 @@ __device__ __forceinline__ int vm_slot(uint32_t w, int ibase) {
   return (w & 0x800000u) ? ix : ibase + ix;
 }
 
+// digits of 256 p
+struct Off256 {
+  uint32_t d[14];
+};
+constexpr Off256 vm_off256() {
+  Off256 o{};
+  uint64_t carry = 0;
+  for (int i = 0; i < 14; i++) {
+    const uint64_t v = ((uint64_t)P29[i] << 8) + carry;
+    o.d[i] = (uint32_t)(v & 0x1fffffffu);
+    carry = v >> 29;
+  }
+  return o;
+}
+constexpr Off256 VM_OFF = vm_off256();
+
+// 256 p again, in a redundant digit form with digits 0..12 >= 2^37 (each
+// 2^37 lent to digit i is taken back as 2^8 from digit i+1): accumulators
+// started here stay non-negative digit by digit (a form's negative mass is
+// at most 190 (2^29 - 1) < 2^37 per digit), so one carry step without a
+// sequential chain normalises them (vm_normalise_fast).
+struct OffR {
+  int64_t d[14];
+};
+constexpr OffR vm_offr() {
+  OffR o{};
+  for (int i = 0; i < 14; i++) {
+    o.d[i] = (int64_t)VM_OFF.d[i];
+    if (i < 13) o.d[i] += (int64_t)1 << 37;
+    if (i > 0) o.d[i] -= 256;
+  }
+  return o;
+}
+constexpr OffR VM_OFFR = vm_offr();
+
 struct Acc {
-  uint32_t l[13];
+  int64_t d[14];
 };
 
-__device__ __forceinline__ void acc_init(Acc& a) {  // 256 p
+__device__ __forceinline__ void vm_lincomb(Acc& acc, const Fd* slots, int ibase, const uint32_t* w, int n) {
 #pragma unroll
-  for (int i = 0; i < 13; i++) {
-    const uint32_t lo = i < 12 ? P_LIMBS[i] : 0u;
-    const uint32_t prev = i > 0 ? P_LIMBS[i - 1] : 0u;
-    a.l[i] = (lo << 8) | (i > 0 ? (prev >> 24) : 0u);
-  }
-}
-
-// acc += c * x for a small signed c (|c| < 128), one carry chain
-__device__ __forceinline__ void acc_term(Acc& acc, const Fp& x, int c) {
-  const uint32_t m = (uint32_t)(c < 0 ? -c : c);
-  uint32_t y[13];
-  if (m == 1u) {
-#pragma unroll
-    for (int i = 0; i < 12; i++) y[i] = x.l[i];
-    y[12] = 0;
-  } else {
-    uint32_t carry = 0;
-#pragma unroll
-    for (int i = 0; i < 12; i++) {
-      const uint64_t t = (uint64_t)x.l[i] * m + carry;
-      y[i] = (uint32_t)t;
-      carry = (uint32_t)(t >> 32);
-    }
-    y[12] = carry;
-  }
-  // subtract as add of the complement with carry-in 1
-  const uint32_t neg = c < 0 ? 0xffffffffu : 0u;
-  unsigned cy = neg & 1u;
-#pragma unroll
-  for (int i = 0; i < 13; i++) acc.l[i] = __builtin_addc(acc.l[i], y[i] ^ neg, cy, &cy);
-}
-
-__device__ __forceinline__ void vm_lincomb(Acc& acc, const Fp* slots, int ibase, const uint32_t* w, int n) {
-  acc_init(acc);
+  for (int i = 0; i < 14; i++) acc.d[i] = VM_OFFR.d[i];
 #pragma unroll
   for (int k = 0; k < VM_MAXT; k++) {
     if (k < n && w[k]) {
-      const Fp x = slots[vm_slot(w[k], ibase)];
-      acc_term(acc, x, (int)(w[k] >> 24) - 128);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const __attribute__((address_space(3))) u32x4* q =
+          (const __attribute__((address_space(3))) u32x4*)(slots + vm_slot(w[k], ibase));
+      u32x4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];  // 4 x ds_read_b128
+      asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));  // keep the loads whole
+      const uint32_t x[14] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, v3.x, v3.y};
+      const int32_t c = (int32_t)(w[k] >> 24) - 128;
+#pragma unroll
+      for (int i = 0; i < 14; i++) acc.d[i] += (int64_t)(int32_t)x[i] * (int64_t)c;
     }
   }
 }
 
-// canonical residue of an accumulator (< 2^390): q = floor(top / (ptop + 1))
-// estimated in double precision (never above floor(a / p)), then up to three
-// conditional subtractions.
-__device__ __forceinline__ Fp vm_reduce(const Acc& a) {
-  const uint64_t top = ((uint64_t)a.l[12] << 34) | ((uint64_t)a.l[11] << 2) | (a.l[10] >> 30);  // a >> 350
-  constexpr uint64_t PTOP = (((uint64_t)P_LIMBS[11]) << 2) | (P_LIMBS[10] >> 30);                // p >> 350
+// carry pass: signed digit sums (total in [0, 2^390)) -> digits < 2^29
+__device__ __forceinline__ void vm_normalise(uint32_t x[14], const Acc& a) {
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const int64_t v = a.d[i] + c;
+    x[i] = (uint32_t)v & 0x1fffffffu;
+    c = v >> 29;
+  }
+}
+
+// one parallel carry step for accumulators with every digit in [0, 2^38):
+// x_i = (a_i mod 2^29) + (a_{i-1} >> 29), i.e. digits < 2^29 + 2^9, which
+// fp_mul_digits_raw accepts (its 64-bit column sums stay below 2^63).
+__device__ __forceinline__ void vm_normalise_fast(uint32_t x[14], const Acc& a) {
+  uint32_t hi_prev = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t lo32 = (uint32_t)a.d[i], hi32 = (uint32_t)((uint64_t)a.d[i] >> 32);
+    if (i < 13) {
+      x[i] = (lo32 & 0x1fffffffu) + hi_prev;
+      hi_prev = __builtin_amdgcn_alignbit(hi32, lo32, 29);
+    } else {
+      x[i] = lo32 + hi_prev;  // the top digit has no high part (value < 2^390)
+    }
+  }
+}
+
+// r - p if r >= p (digits < 2^29, r < 2p)
+__device__ __forceinline__ void vm_reduce_once(uint32_t r[14]) {
+  uint32_t t[14];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const int32_t v = (int32_t)r[i] - (int32_t)P29[i] - br;
+    t[i] = (uint32_t)v & 0x1fffffffu;
+    br = v < 0 ? 1 : 0;
+  }
+  const bool keep = br != 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r[i] = keep ? r[i] : t[i];
+}
+
+// canonical residue of a normalised value x < 2^390: q = floor(top / (ptop + 1))
+// estimated in double precision (never above floor(x / p)), x - q p by one
+// more digit pass, then up to two conditional subtractions.
+__device__ __forceinline__ void vm_reduce(uint32_t x[14]) {
+  const uint64_t top = ((uint64_t)x[13] << 27) | (x[12] >> 2);  // x >> 350
+  constexpr uint64_t PTOP = (((uint64_t)P_LIMBS[11]) << 2) | (P_LIMBS[10] >> 30);
   constexpr double INV = 1.0 / (double)(PTOP + 1);
   const double qd = (double)top * INV - 1e-6;
-  const uint32_t q = qd > 0.0 ? (uint32_t)qd : 0u;
-  uint32_t r[13];
-  uint32_t carry = 0;
-  unsigned b = 0;
+  const int32_t q = qd > 0.0 ? (int32_t)qd : 0;
+  Acc a;
 #pragma unroll
-  for (int i = 0; i < 13; i++) {
-    const uint64_t t = (uint64_t)(i < 12 ? P_LIMBS[i] : 0u) * q + carry;
-    carry = (uint32_t)(t >> 32);
-    r[i] = __builtin_subc(a.l[i], (uint32_t)t, b, &b);
-  }
-  Fp v;
-#pragma unroll
-  for (int i = 0; i < 12; i++) v.l[i] = r[i];
-  v = fp_reduce_once(v);
-  v = fp_reduce_once(v);
-  v = fp_reduce_once(v);
-  return v;
+  for (int i = 0; i < 14; i++) a.d[i] = (int64_t)x[i] - (int64_t)q * (int64_t)P29[i];
+  vm_normalise(x, a);
+  vm_reduce_once(x);
+  vm_reduce_once(x);
 }
 
 // Load up to VM_MAXT term words (predicated; all loads issued together).
@@ -126,7 +197,7 @@ __device__ __forceinline__ void vm_load_terms(uint32_t* w, const uint32_t* src, 
 // pred[g]: per-item predicate (sel: bit 0) or table index (lut).  All 64
 // lanes of the workgroup must call it.
 template <int G>
-__device__ __noinline__ void vm_run(const VmProg p, Fp* slots, int item0, int stride, const uint32_t* pred) {
+__device__ __noinline__ void vm_run(const VmProg p, Fd* slots, int item0, int stride, const uint32_t* pred) {
   const int lane = threadIdx.x;
   for (int lv = 0; lv < p.nlevels; lv++) {
     const uint32_t nitems = p.levels[lv][0], na = p.levels[lv][1], nb = p.levels[lv][2], base = p.levels[lv][3];
@@ -137,18 +208,24 @@ __device__ __noinline__ void vm_run(const VmProg p, Fp* slots, int item0, int st
       const uint32_t* t = p.terms + base + j * sw;
       const uint32_t d = t[0];
       const uint32_t kind = d >> 30;
-      uint32_t wa[VM_MAXT], wb[VM_MAXT];
-      Fp out;
+      uint32_t wa[VM_MAXT];
+      Fd out;
       if (kind == 1u) {  // mul
-        vm_load_terms(wa, t + 1, (int)na);
-        vm_load_terms(wb, t + 1 + na, (int)nb);
-        Acc a, b;
-        vm_lincomb(a, slots, ibase, wa, (int)na);
-        vm_lincomb(b, slots, ibase, wb, (int)nb);
         uint32_t x[14], y[14];
-        fp_unpack29_wide(x, a.l);
-        fp_unpack29_wide(y, b.l);
-        out = fp_mul_digits(x, y);
+        {
+          vm_load_terms(wa, t + 1, (int)na);
+          Acc a;
+          vm_lincomb(a, slots, ibase, wa, (int)na);
+          vm_normalise_fast(x, a);
+        }
+        {
+          vm_load_terms(wa, t + 1 + na, (int)nb);
+          Acc b;
+          vm_lincomb(b, slots, ibase, wa, (int)nb);
+          vm_normalise_fast(y, b);
+        }
+        fp_mul_digits_raw(out.d, x, y);
+        vm_reduce_once(out.d);
       } else if (kind == 3u) {  // lut
         const uint32_t w = t[1];
         const int stride_t = (int)(w >> 24) - 128;
@@ -160,8 +237,11 @@ __device__ __noinline__ void vm_run(const VmProg p, Fp* slots, int item0, int st
         vm_load_terms(wa, src, n);
         Acc a;
         vm_lincomb(a, slots, ibase, wa, n);
-        out = vm_reduce(a);
+        vm_normalise(out.d, a);
+        vm_reduce(out.d);
       }
+      out.d[14] = 0;
+      out.d[15] = 0;
       slots[vm_slot(d & 0x3fffffffu, ibase)] = out;
     }
     __syncthreads();
@@ -169,11 +249,11 @@ __device__ __noinline__ void vm_run(const VmProg p, Fp* slots, int item0, int st
 }
 
 // Constant pool -> slots[0 .. WP_NCONST)
-__device__ __forceinline__ void vm_load_consts(Fp* slots) {
+__device__ __forceinline__ void vm_load_consts(Fd* slots) {
   for (int i = threadIdx.x; i < WP_NCONST; i += VM_NT) {
-    Fp v;
+    Fd v;
 #pragma unroll
-    for (int k = 0; k < 12; k++) v.l[k] = WP_CONST_POOL[i].l[k];
+    for (int k = 0; k < 16; k++) v.d[k] = WP_CONST_POOL[i].d[k];
     slots[i] = v;
   }
   __syncthreads();

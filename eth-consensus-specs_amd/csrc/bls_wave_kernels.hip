@@ -23,8 +23,8 @@ __device__ __forceinline__ Fp& fp12_slot_dst(Fp12& f, int j) {
 }
 
 // lanes 0..11 load/store one coefficient each
-__device__ __forceinline__ void load_fp12(Fp* dst, const Fp12* src) {
-  if (threadIdx.x < 12) dst[threadIdx.x] = fp12_slot_src(*src, threadIdx.x);
+__device__ __forceinline__ void load_fp12(Fd* dst, const Fp12* src) {
+  if (threadIdx.x < 12) dst[threadIdx.x] = fd_from_fp(fp12_slot_src(*src, threadIdx.x));
   __syncthreads();
 }
 
@@ -36,7 +36,7 @@ constexpr int ML_G = 2;  // pairs per workgroup
 
 template <int G>
 __global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* fout) {
-  __shared__ Fp slots[WP_NCONST + G * WL_ML_STRIDE];
+  __shared__ Fd slots[WP_NCONST + G * WL_ML_STRIDE];
   __shared__ int skip[G];
   const int lane = threadIdx.x;
   const size_t i0 = (size_t)blockIdx.x * G;
@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q,
   for (int k = lane; k < 12 * G; k += 64) {
     const int g = k / 12, j = k % 12;
     const size_t i = i0 + g;
-    Fp* r = slots + item0 + g * WL_ML_STRIDE;
+    Fd* r = slots + item0 + g * WL_ML_STRIDE;
     Fp v = fp_zero();
     if (!skip[g]) {
       const G2A& q = Q[i];
@@ -61,9 +61,9 @@ __global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q,
       else if (j == 7) v = P[i].y;
       else if (j >= 8) v = (j & 1) ? (j < 10 ? q.x.c1 : q.y.c1) : (j < 10 ? q.x.c0 : q.y.c0);
     }
-    if (j < 6) r[WL_ML_T + j] = v;
-    else if (j < 8) r[WL_ML_P + j - 6] = v;
-    else r[WL_ML_Q + j - 8] = v;
+    if (j < 6) r[WL_ML_T + j] = fd_from_fp(v);
+    else if (j < 8) r[WL_ML_P + j - 6] = fd_from_fp(v);
+    else r[WL_ML_Q + j - 8] = fd_from_fp(v);
   }
   __syncthreads();
   vm_run<G>(VM_PROG(ML_DBL_FIRST), slots, item0, WL_ML_STRIDE, nullptr);
@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q,
     const int g = k / 12, j = k % 12;
     const size_t i = i0 + g;
     if (i >= n) continue;
-    Fp v = slots[item0 + g * WL_ML_STRIDE + WL_ML_F + j];
+    Fp v = fp_from_fd(slots[item0 + g * WL_ML_STRIDE + WL_ML_F + j]);
     if ((j >> 1) & 1) v = fp_neg(v);
     if (skip[g]) v = j == 0 ? FP_ONE : fp_zero();
     fp12_slot_dst(fout[i], j) = v;
@@ -87,21 +87,21 @@ __global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q,
 // ============================================ Fp12 registers of one item ==
 // Region WL_FE_*: registers R0..R6 (12 slots each) | scratch.  Every
 // operation is a program instance bound to its registers (FE_* in wavec).
-__device__ __forceinline__ Fp* fe_reg(Fp* s, int k) { return s + WP_NCONST + 12 * k; }
-__device__ __forceinline__ void fe_run(Fp* s, const VmProg p) { vm_run<1>(p, s, WP_NCONST, 0, nullptr); }
-__device__ __forceinline__ void fe_copy(Fp* s, int dst, int a) {
+__device__ __forceinline__ Fd* fe_reg(Fd* s, int k) { return s + WP_NCONST + 12 * k; }
+__device__ __forceinline__ void fe_run(Fd* s, const VmProg p) { vm_run<1>(p, s, WP_NCONST, 0, nullptr); }
+__device__ __forceinline__ void fe_copy(Fd* s, int dst, int a) {
   if (threadIdx.x < 12) fe_reg(s, dst)[threadIdx.x] = fe_reg(s, a)[threadIdx.x];
   __syncthreads();
 }
-__device__ __forceinline__ void fe_conj(Fp* s, int dst, int a) {
+__device__ __forceinline__ void fe_conj(Fd* s, int dst, int a) {
   if (threadIdx.x < 12) {
-    const Fp v = fe_reg(s, a)[threadIdx.x];
-    fe_reg(s, dst)[threadIdx.x] = ((threadIdx.x >> 1) & 1) ? fp_neg(v) : v;
+    const Fp v = fp_from_fd(fe_reg(s, a)[threadIdx.x]);
+    fe_reg(s, dst)[threadIdx.x] = fd_from_fp(((threadIdx.x >> 1) & 1) ? fp_neg(v) : v);
   }
   __syncthreads();
 }
 // R1 = R2^x (x = -|x|; cyclotomic input, so the inverse is the conjugate)
-__device__ void fe_pow_x(Fp* s) {
+__device__ void fe_pow_x(Fd* s) {
   fe_run(s, VM_PROG(FE_POWX_0));
   fe_run(s, VM_PROG(FE_POWX_1));
   fe_run(s, VM_PROG(FE_POWX_2));
@@ -115,7 +115,7 @@ __device__ void fe_pow_x(Fp* s) {
 // Easy part (p^6-1)(p^2+1); hard part via (x-1)^2 (x+p) (x^2+p^2-1) + 3, which
 // returns e^3 (e == 1 <=> e^3 == 1 since gcd(3, r) = 1).
 __global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, int* out) {
-  __shared__ Fp s[WP_NCONST + WL_FE_STRIDE];
+  __shared__ Fd s[WP_NCONST + WL_FE_STRIDE];
   __shared__ Fp12 inv;
   __shared__ int okc;
   const int lane = threadIdx.x;
@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, i
   }
   if (lane == 0) {
     Fp12 f;
-    for (int j = 0; j < 12; j++) fp12_slot_dst(f, j) = fe_reg(s, 0)[j];
+    for (int j = 0; j < 12; j++) fp12_slot_dst(f, j) = fp_from_fd(fe_reg(s, 0)[j]);
     inv = fp12_inv(f);
   }
   __syncthreads();
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, i
   if (lane == 0) okc = 1;
   __syncthreads();
   if (lane < 12) {
-    const Fp v = fe_reg(s, 1)[lane];
+    const Fp v = fp_from_fd(fe_reg(s, 1)[lane]);
     const bool good = lane == 0 ? fp_is_one(v) : fp_is_zero(v);
     if (!good) okc = 0;
   }
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, i
 
 // Products of consecutive chunks: out[b] = prod in[b*chunk .. min(n, (b+1)*chunk))
 __global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n, int chunk, Fp12* outp) {
-  __shared__ Fp s[WP_NCONST + WL_CH_STRIDE];
+  __shared__ Fd s[WP_NCONST + WL_CH_STRIDE];
   const size_t lo = (size_t)blockIdx.x * chunk;
   const size_t hi = lo + chunk < n ? lo + chunk : n;
   vm_load_consts(s);
@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n
     load_fp12(s + base + 12, in + i);
     vm_run<1>(VM_PROG(CH_MUL), s, base, 0, nullptr);
   }
-  if (threadIdx.x < 12) fp12_slot_dst(outp[blockIdx.x], threadIdx.x) = s[base + threadIdx.x];
+  if (threadIdx.x < 12) fp12_slot_dst(outp[blockIdx.x], threadIdx.x) = fp_from_fd(s[base + threadIdx.x]);
 }
 
 static int env_int(const char* name, int dflt) {

@@ -56,6 +56,49 @@ __global__ void __launch_bounds__(256) mul_lo_chains(uint64_t* out, int iters, u
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// 8 independent chains of v_mad_i64_i32 (signed 32x32+64)
+__global__ void __launch_bounds__(256) madi_chains(uint64_t* out, int iters, uint32_t a, uint32_t b) {
+  uint64_t acc[8];
+  for (int k = 0; k < 8; k++) acc[k] = threadIdx.x + k;
+  uint32_t x = a + threadIdx.x, y = b ^ blockIdx.x;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      { uint64_t cc; asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(cc) : "v"(x), "v"(y)); }
+    }
+  }
+  uint64_t s = 0;
+  for (int k = 0; k < 8; k++) s ^= acc[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// 8 independent chains of v_add_co_u32 + v_addc_co_u32 (a 64-bit add as 2 ops)
+__global__ void __launch_bounds__(256) addc_chains(uint64_t* out, int iters, uint32_t a, uint32_t b) {
+  uint32_t lo[8], hi[8];
+  for (int k = 0; k < 8; k++) { lo[k] = threadIdx.x + k; hi[k] = k; }
+  uint32_t x = a + threadIdx.x;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      asm volatile("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, %1, %2, vcc" : "+v"(lo[k]), "+v"(hi[k]) : "v"(x) : "vcc");
+  }
+  uint32_t s = 0;
+  for (int k = 0; k < 8; k++) s ^= lo[k] ^ hi[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// 8 independent v_lshl_add_u64 chains (64-bit add in one op)
+__global__ void __launch_bounds__(256) add64_chains(uint64_t* out, int iters, uint32_t a, uint32_t b) {
+  uint64_t acc[8];
+  for (int k = 0; k < 8; k++) acc[k] = threadIdx.x + k;
+  uint64_t x = a + threadIdx.x;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) asm volatile("v_lshl_add_u64 %0, %1, 0, %0" : "+v"(acc[k]) : "v"(x));
+  }
+  uint64_t s = 0;
+  for (int k = 0; k < 8; k++) s ^= acc[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 struct Fp { uint32_t v[12]; };
 __constant__ uint32_t P[12] = {0xffffaaab,0xb9feffff,0xb153ffff,0x1eabfffe,0xf6b0f624,0x6730d2a0,0xf38512bf,0x64774b84,0x434bacd7,0x4b1ba7b6,0x397fe69a,0x1a0111ea};
 #define NINV 0xfffcfffdu
@@ -101,8 +144,10 @@ int main() {
   const int iters = 4096;
   struct { const char* name; void (*k)(uint64_t*, int, uint32_t, uint32_t); } ks[] = {
     {"v_mad_u64_u32 x8 indep", mad_chains}, {"v_mad_u64_u32 dependent", mad_dep},
+    {"v_mad_i64_i32 x8 indep", madi_chains}, {"v_add_co+addc x8 (2 ops)", addc_chains},
+    {"v_lshl_add_u64 x8 indep", add64_chains},
     {"v_add_u32 x8 indep", add_chains}, {"v_mul_lo_u32 x8 indep", mul_lo_chains}, {"montmul (x8 = FME/8)", montmul_k}};
-  int grids[] = {256, 1024, 2048, 4096};
+  int grids[] = {1024, 4096};
   for (auto& K : ks) {
     for (int g : grids) {
       hipLaunchKernelGGL(K.k, dim3(g), dim3(256), 0, 0, d, 16, 3u, 5u);

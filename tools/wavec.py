@@ -1091,11 +1091,11 @@ def emit(progs, path):
         out.append("")
     pool = sorted(CONST_POOL.items(), key=lambda kv: kv[1])
     rows = []
-    for v, _ in pool:
+    for v, _ in pool:  # Montgomery form (R = 2^406) as 14 radix-2^29 digits + 2 pad words
         m = v * (1 << 406) % P
-        rows.append("{{" + ", ".join("0x%08xu" % ((m >> (32 * i)) & 0xFFFFFFFF) for i in range(12)) + "}}")
+        rows.append("{{" + ", ".join("0x%08xu" % ((m >> (29 * i)) & 0x1FFFFFFF) for i in range(14)) + ", 0u, 0u}}")
     out.append(f"static constexpr int WP_NCONST = {len(pool)};")
-    out.append("struct WpConst { uint32_t l[12]; };")
+    out.append("struct WpConst { uint32_t d[16]; };")
     out.append(f"static constexpr WpConst WP_CONST_POOL[{max(1, len(pool))}] = {{{', '.join(rows or ['{{0}}'])}}};")
     out.append("")
     out.append("}  // namespace bls")
