@@ -18,7 +18,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC,
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF,
   NSLOT
 };
 
@@ -33,7 +33,8 @@ struct bls_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // concurrent branch of the FAV batch (hash_to_G2)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t stream3 = nullptr;  // concurrent branch: sum r_i sigma_i (MSM) + its Miller loop
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sig = nullptr, ev_msm = nullptr;
   std::mutex mu;
   std::string err;
   Buf buf[NSLOT];
@@ -53,7 +54,8 @@ struct bls_ctx {
 };
 
 static const char* const PROF_NAMES[] = {"fav_gather", "sig_decode", "fav_hash", "g2_sum",        "sig_pair", "miller",
-                                         "fp12_prod",  "final_exp",  "fav_finish", "partials_prod", "sig_vm"};
+                                         "fp12_prod",  "final_exp",  "fav_finish", "partials_prod", "sig_vm",
+                                         "msm"};
 static const int PROF_N = sizeof(PROF_NAMES) / sizeof(PROF_NAMES[0]);
 
 namespace {
@@ -220,10 +222,15 @@ int bls_ctx_create(int device, bls_ctx** out) {
   bls_ctx* c = new (std::nothrow) bls_ctx();
   if (!c) return BLS_E_DEVICE;
   c->device = device;
+  int prio_lo = 0, prio_hi = 0;  // the MSM branch is latency-bound: schedule it first
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_sig, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_msm, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return BLS_E_DEVICE;
   }
@@ -245,9 +252,13 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   if (ctx->reg) (void)hipFree(ctx->reg);
   if (ctx->reg_ok) (void)hipFree(ctx->reg_ok);
   (void)hipStreamSynchronize(ctx->stream2);
+  (void)hipStreamSynchronize(ctx->stream3);
   (void)hipEventDestroy(ctx->ev_fork);
   (void)hipEventDestroy(ctx->ev_join);
+  (void)hipEventDestroy(ctx->ev_sig);
+  (void)hipEventDestroy(ctx->ev_msm);
   (void)hipStreamDestroy(ctx->stream2);
+  (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -583,45 +594,56 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   G1J* apk;
   int *status, *flag;
   G1A *apka, *rP;
-  G2A *sig, *H;
-  G2J *rS, *tmp, *S;
+  G2A *sig, *H, *saff;
   Fp12 *f, *ft, *fo;
   Fp* U;
+  Fd* msmf;
   uint64_t* rsc;
+  uint32_t* msmu;
   uint8_t* d_seed;
   SCR(S_APK, B, apk);
   SCR(S_STATUS, B + 1, status);
   SCR(S_APKA, B, apka);
   SCR(S_SIG, B, sig);
   SCR(S_RP, B + 1, rP);
-  SCR(S_RS, B, rS);
-  SCR(S_H, B + 1, H);
+  SCR(S_H, B, H);
   SCR(S_U, 8 * B, U);
   SCR(S_FLAG, B, flag);
   SCR(S_RSC, B, rsc);
-  SCR(S_G2J_T, 1024, tmp);
-  SCR(S_G2J, 1, S);
-  SCR(S_F, B + 1, f);
+  SCR(S_MSMU, msm_scratch_u32(B), msmu);
+  SCR(S_MSMF, msm_scratch_fd(), msmf);
+  SCR(S_SAFF, 1, saff);
+  SCR(S_F, B + 2, f);
   SCR(S_F_T, (B + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
-  hipStream_t st = ctx->stream;
-  // fork: hash_to_G2 of every message runs on stream2 beside the gather /
-  // signature branch; both join before the Miller loops.
+  hipStream_t st = ctx->stream, st2 = ctx->stream2, st3 = ctx->stream3;
+  // stream2: hash_to_G2 of every message, beside the gather / signature branch
   HIPCK(hipEventRecord(ctx->ev_fork, st));
-  HIPCK(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-  PROF2(2, ctx->stream2, launch_h2c(ctx->stream2, B, d_msgs, nullptr, U, H, flag));
-  HIPCK(hipEventRecord(ctx->ev_join, ctx->stream2));
+  HIPCK(hipStreamWaitEvent(st2, ctx->ev_fork, 0));
+  PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, H, flag));
+  HIPCK(hipEventRecord(ctx->ev_join, st2));
   PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
   PROF(1, launch_sig_decode(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rsc));
-  PROF(10, launch_sig_vm(st, B, status, apka, sig, rsc, rP, rS));
-  PROF(3, launch_g2_sum_jac(st, rS, B, tmp, S));
-  PROF(4, launch_sig_pair(st, S, rP + B, H + B));
-  HIPCK(hipMemsetD32Async((hipDeviceptr_t)(status + B), 1, 1, st));
+  PROF(10, launch_sig_vm(st, B, status, apka, sig, rsc, rP));
+  HIPCK(hipEventRecord(ctx->ev_sig, st));
+  // stream3: S = sum r_i sigma_i and the Miller loop of (-G1, S) -> f[B + 1]
+  HIPCK(hipStreamWaitEvent(st3, ctx->ev_sig, 0));
+  {
+    ProfScope ps_(ctx, 11, st3);
+    LK(launch_msm(st3, B, status, rsc, sig, msmu, msmf, saff));
+    hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, rP + B);
+    LK(hipGetLastError());
+    LK(launch_miller_wave(st3, rP + B, saff, nullptr, 1, f + B + 1));
+  }
+  HIPCK(hipEventRecord(ctx->ev_msm, st3));
+  // stream1: Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-  PROF(5, launch_miller_wave(st, rP, H, status, B + 1, f));
-  PROF(6, launch_fp12_prod_vm(st, f, B + 1, ft, fo));
+  PROF(5, launch_miller_wave(st, rP, H, status, B, f));
+  PROF(6, launch_fp12_prod_vm(st, f, B, ft, f + B));
+  HIPCK(hipStreamWaitEvent(st, ctx->ev_msm, 0));
+  LK(launch_fp12_prod_vm(st, f + B, 2, ft, fo));
   ctx->fav_B = B;
   ctx->fav_ready = true;
   *out_f = fo;

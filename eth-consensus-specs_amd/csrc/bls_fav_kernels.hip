@@ -4,9 +4,9 @@
 //     symbols), signature decompression, RLC scalars;
 //   - wave-program kernels (bls_vm.h, G items per 64-lane workgroup) for the
 //     point arithmetic: 3-isogeny + cofactor clearing of hash_to_G2, and the
-//     three signature-side chains ([|x|] sigma for the subgroup check,
-//     r * apk in G1, r * sigma in G2) advanced together one scalar bit per
-//     step with complete (exception-free) projective formulas.
+//     two per-item signature-side chains ([|x|] sigma for the subgroup check
+//     and r * apk in G1) advanced together one scalar bit per step with
+//     complete (exception-free) projective formulas.
 #include "bls_kernels.h"
 #include "bls_lane.h"
 #include "bls_vm.h"
@@ -149,11 +149,12 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
   status[i] = st;
 }
 
-// (2) the three signature-side chains, 64 steps, then the subgroup verdict,
-// r * apk to affine and r * sigma to Jacobian.
+// (2) the two per-item signature-side chains, 64 steps ([|x|] sigma for the
+// subgroup check and r * apk), then the subgroup verdict and r * apk to
+// affine.  sum r_i sigma_i is the batch MSM (bls_msm.hip).
 template <int G>
 __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G1A* apk_aff, const G2A* sig,
-                                                 const uint64_t* rsc, G1A* rP, G2J* rS) {
+                                                 const uint64_t* rsc, G1A* rP) {
   __shared__ Fd s[WP_NCONST + G * WL_SG_STRIDE];
   __shared__ int live[G];
   __shared__ uint32_t pred[G];
@@ -168,9 +169,9 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
   }
   __syncthreads();
   const int item0 = WP_NCONST;
-  // sigma (4) | apk (2) | M = (sigma, 1) (6) | R = (0:1:0) (3) | S = (0:1:0) (6)
-  for (int k = lane; k < 21 * G; k += 64) {
-    const int g = k / 21, j = k % 21;
+  // sigma (4) | apk (2) | M = (sigma, 1) (6) | R = (0:1:0) (3)
+  for (int k = lane; k < 15 * G; k += 64) {
+    const int g = k / 15, j = k % 15;
     const size_t i = i0 + g;
     Fp v = fp_zero();
     if (live[g]) {
@@ -180,7 +181,7 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
       else if (j < 10) v = j == 6 ? q.x.c0 : (j == 7 ? q.x.c1 : (j == 8 ? q.y.c0 : q.y.c1));
       else if (j == 10) v = FP_ONE;
     }
-    if (j == 13 || j == 17) v = FP_ONE;  // Y of R and Re Y of S
+    if (j == 13) v = FP_ONE;  // Y of R
     s[item0 + g * WL_SG_STRIDE + j] = fd_from_fp(v);
   }
   __syncthreads();
@@ -201,7 +202,6 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
   }
   __syncthreads();
   vm_run<G>(VM_PROG(SG_TOAFF), s, item0, WL_SG_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(SG_TOJAC), s, item0, WL_SG_STRIDE, nullptr);
   if (lane < G) {
     const size_t i = i0 + lane;
     if (i < B) {
@@ -210,17 +210,7 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
       // sigma in G2  <=>  psi(sigma) == -[|x|] sigma  (differences zero, M not the identity)
       for (int j = 0; j < 4; j++) ok = ok && fd_is_zero(e[WL_SG_D + j]);
       ok = ok && !(fd_is_zero(e[WL_SG_D + 4]) && fd_is_zero(e[WL_SG_D + 5]));
-      if (ok) {
-        rP[i] = G1A{fp_from_fd(e[WL_SG_XY1]), fp_from_fd(e[WL_SG_XY1 + 1]), false};
-        G2J j;
-        j.x = Fp2{fp_from_fd(e[WL_SG_SJ]), fp_from_fd(e[WL_SG_SJ + 1])};
-        j.y = Fp2{fp_from_fd(e[WL_SG_SJ + 2]), fp_from_fd(e[WL_SG_SJ + 3])};
-        j.z = Fp2{fp_from_fd(e[WL_SG_SJ + 4]), fp_from_fd(e[WL_SG_SJ + 5])};
-        rS[i] = j;
-      } else {
-        rP[i] = G1A{fp_zero(), fp_zero(), true};
-        rS[i] = jac_identity<Fp2>();
-      }
+      rP[i] = ok ? G1A{fp_from_fd(e[WL_SG_XY1]), fp_from_fd(e[WL_SG_XY1 + 1]), false} : G1A{fp_zero(), fp_zero(), true};
       status[i] = ok ? 1 : 0;
     }
   }
@@ -250,9 +240,9 @@ hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, co
 }
 
 hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const G1A* apk_aff, const G2A* sig,
-                         const uint64_t* rsc, G1A* rP, G2J* rS) {
+                         const uint64_t* rsc, G1A* rP) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_vm<FAV_G>, dim3(nblk(B, FAV_G)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP, rS);
+  hipLaunchKernelGGL(k_sig_vm<FAV_G>, dim3(nblk(B, FAV_G)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
   return hipGetLastError();
 }
 

@@ -17,6 +17,11 @@ namespace bls {
 struct alignas(16) Fp {
   uint32_t l[12];
 };
+// VM slot form of an Fp value (bls_vm.h): 14 radix-2^29 digits + 2 zero pad
+// words (64 B), canonical residue in Montgomery form.
+struct alignas(16) Fd {
+  uint32_t d[16];
+};
 struct Fp2 {
   Fp c0, c1;  // c0 + c1 * i,  i^2 = -1
 };

@@ -27,10 +27,6 @@ namespace bls {
 constexpr int VM_MAXT = 12;  // wavec MAX_TERMS
 constexpr int VM_NT = 64;    // lanes per workgroup
 
-struct alignas(16) Fd {
-  uint32_t d[16];  // d[0..13]: radix-2^29 digits; d[14..15] = 0
-};
-
 BLS_HD Fd fd_from_fp(const Fp& a) {
   Fd r;
   fp_unpack29(r.d, a);
@@ -108,19 +104,22 @@ struct Acc {
   int64_t d[14];
 };
 
+// n is uniform across the wave (the level's operand width); padding words
+// (0) read slot ibase with coefficient 0, so the loop body has no
+// lane-dependent branch and loads of term k+1 can overlap the mads of term k.
 __device__ __forceinline__ void vm_lincomb(Acc& acc, const Fd* slots, int ibase, const uint32_t* w, int n) {
 #pragma unroll
   for (int i = 0; i < 14; i++) acc.d[i] = VM_OFFR.d[i];
 #pragma unroll
   for (int k = 0; k < VM_MAXT; k++) {
-    if (k < n && w[k]) {
+    if (k < n) {
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       const __attribute__((address_space(3))) u32x4* q =
           (const __attribute__((address_space(3))) u32x4*)(slots + vm_slot(w[k], ibase));
       u32x4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];  // 4 x ds_read_b128
       asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));  // keep the loads whole
       const uint32_t x[14] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, v3.x, v3.y};
-      const int32_t c = (int32_t)(w[k] >> 24) - 128;
+      const int32_t c = w[k] ? (int32_t)(w[k] >> 24) - 128 : 0;
 #pragma unroll
       for (int i = 0; i < 14; i++) acc.d[i] += (int64_t)(int32_t)x[i] * (int64_t)c;
     }
@@ -234,9 +233,9 @@ __device__ __noinline__ void vm_run(const VmProg p, Fd* slots, int item0, int st
         const bool pick_b = kind == 2u && !(pred[g] & 1u);
         const uint32_t* src = pick_b ? t + 1 + na : t + 1;
         const int n = pick_b ? (int)nb : (int)na;
-        vm_load_terms(wa, src, n);
+        vm_load_terms(wa, src, n);  // zero-filled past this op's own list
         Acc a;
-        vm_lincomb(a, slots, ibase, wa, n);
+        vm_lincomb(a, slots, ibase, wa, (int)(na > nb ? na : nb));  // uniform bound
         vm_normalise(out.d, a);
         vm_reduce(out.d);
       }

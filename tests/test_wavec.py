@@ -251,22 +251,46 @@ def test_g1_to_affine_program():
 
 
 def test_signature_step_programs():
-    """64 steps of SIG_STEP{0,1,2}: M = [|x|] sigma, R = r apk, S = r sigma."""
+    """64 steps of SIG_STEP{0,1,2}: M = [|x|] sigma, R = r apk."""
     sig = O.g2_mul(O.G2_GEN, 0x1234_5678_9ABC)
     apk = O.g1_mul(O.G1_GEN, 0xDEADBEEF)
     r = rng.getrandbits(64) | (1 << 63)
     fr = [[sig[0][0], sig[0][1], sig[1][0], sig[1][1]], [apk[0], apk[1]],
-          [sig[0][0], sig[0][1], sig[1][0], sig[1][1], 1, 0], g1_proj(None), g2_proj(None)]
+          [sig[0][0], sig[0][1], sig[1][0], sig[1][1], 1, 0], g1_proj(None)]
     for b in range(63, -1, -1):
         mode = 0 if b == 63 else (2 if (O.X_ABS >> b) & 1 else 1)
-        fr = run(PROGS[f"SIG_STEP{mode}"], fr, pred=(r >> b) & 1)[:5]
+        fr = run(PROGS[f"SIG_STEP{mode}"], fr, pred=(r >> b) & 1)[:4]
     assert g2_aff(fr[2]) == O.g2_mul(sig, O.X_ABS)
     assert g1_aff(fr[3]) == O.g1_mul(apk, r)
-    assert g2_aff(fr[4]) == O.g2_mul(sig, r)
     out = run(PROGS["G2_SUBCHK"], [fr[0], fr[2], [0] * 6])[2]
     assert out[:4] == [0, 0, 0, 0] and out[4:6] != [0, 0]
-    jac = run(PROGS["G2_PROJ2JAC"], [fr[4], [0] * 6])[1]
-    z = (jac[4], jac[5])
-    zi = O.f2_inv(z)
-    zi2 = O.f2_mul(zi, zi)
-    assert (O.f2_mul((jac[0], jac[1]), zi2), O.f2_mul((jac[2], jac[3]), O.f2_mul(zi2, zi))) == O.g2_mul(sig, r)
+
+
+def test_msm_programs_pippenger():
+    """Bucket accumulation (G2_ADDAFF_SEL), window running sums (RUNSUM) and
+    the 2^8 Horner steps (G2X_8A) compute sum r_i sigma_i for 8-bit windows."""
+    pts = [O.g2_mul(O.G2_GEN, 1000 + 17 * i) for i in range(5)]
+    rs = [rng.getrandbits(64) for _ in pts]
+    rs[0] = 0x0101010101010101  # repeated digits share buckets
+    windows = []
+    for w in range(8):
+        buckets = {}
+        for p_, r in zip(pts, rs):
+            d = (r >> (8 * w)) & 0xFF
+            if d:
+                buckets.setdefault(d, []).append(p_)
+        T, S = g2_proj(None), g2_proj(None)
+        for d in range(255, 0, -1):
+            B = g2_proj(None)
+            for q in buckets.get(d, []):
+                B = run(PROGS["G2_ADDAFF_SEL"], [B, [q[0][0], q[0][1], q[1][0], q[1][1]]], pred=1)[0]
+            B = run(PROGS["G2_ADDAFF_SEL"], [B, [1, 2, 3, 4]], pred=0)[0]  # skipped step
+            T, S = run(PROGS["RUNSUM"], [T, S, B])[:2]
+        windows.append(S)
+    W = windows[7]
+    for w in range(6, -1, -1):
+        W = run(PROGS["G2X_8A"], [W, windows[w], [0] * 6])[2]
+    expect = None
+    for p_, r in zip(pts, rs):
+        expect = O.g2_add(expect, O.g2_mul(p_, r))
+    assert g2_aff(W) == expect

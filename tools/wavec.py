@@ -741,13 +741,13 @@ def prog_fp2_inv_finish(c):
 
 
 def make_sig_step(mode):
-    """One bit step of the three signature-side chains of an FAV item:
+    """One bit step of the two per-item signature-side chains of an FAV item:
       frame 0: sigma affine (x, y)          frame 1: apk affine (x, y)
       frame 2: M (projective, [|x|] sigma chain)
-      frame 3: R (G1 projective, r * apk)   frame 4: S (G2 projective, r * sigma)
-    R <- pred ? 2R + apk : 2R and S <- pred ? 2S + sigma : 2S (pred = bit of
-    the item's RLC scalar); M <- 2M (mode 1), 2M + sigma (mode 2), unchanged
-    (mode 0, the leading bit)."""
+      frame 3: R (G1 projective, r * apk)
+    R <- pred ? 2R + apk : 2R (pred = bit of the item's RLC scalar);
+    M <- 2M (mode 1), 2M + sigma (mode 2), unchanged (mode 0, the leading
+    bit).  sum r_i sigma_i is a batch MSM (bls_msm.hip)."""
 
     def prog(c):
         sig = (f2_from_frame(c, 0, 0), f2_from_frame(c, 0, 2))
@@ -762,13 +762,27 @@ def make_sig_step(mode):
         D = rcb_dbl(R, B1_3)
         A = rcb_add_aff(D, apk, B1_3)
         out[3] = [sel(c, a, d) for a, d in zip(pt_out(A), pt_out(D))]
-        S = pt_from_frame(c, 4, 0, True)
-        D2 = rcb_dbl(S, B2_3)
-        A2 = rcb_add_aff(D2, sig, B2_3)
-        out[4] = [sel(c, a, d) for a, d in zip(pt_out(A2), pt_out(D2))]
         return out
 
     return prog
+
+
+def prog_g2_add_aff_sel(c):
+    """MSM bucket step: frame 0: R (projective), frame 1: Q (affine);
+    R <- pred ? R + Q : R."""
+    R = pt_from_frame(c, 0, 0, True)
+    Q = (f2_from_frame(c, 1, 0), f2_from_frame(c, 1, 2))
+    S = rcb_add_aff(R, Q, B2_3)
+    return {0: [sel(c, a, b) for a, b in zip(pt_out(S), pt_out(R))]}
+
+
+def prog_runsum(c):
+    """MSM window reduction step: frame 0: T, frame 1: S, frame 2: B (all
+    projective); T <- T + B, S <- S + T  (visiting buckets d = 255 .. 1 gives
+    S = sum d B_d)."""
+    T = rcb_add(pt_from_frame(c, 0, 0, True), pt_from_frame(c, 2, 0, True), B2_3)
+    S = rcb_add(pt_from_frame(c, 1, 0, True), T, B2_3)
+    return {0: pt_out(T), 1: pt_out(S)}
 
 
 def prog_g2_proj_to_jac(c):
@@ -800,9 +814,13 @@ PROGRAMS = {
     "G1_TOAFF": (prog_proj_to_aff1, [3, 1, 2]),
     "FP2_NORM": (prog_fp2_norm, [2, 1]),
     "FP2_INVFIN": (prog_fp2_inv_finish, [2, 1, 2]),
-    "SIG_STEP0": (make_sig_step(0), [4, 2, 6, 3, 6]),
-    "SIG_STEP1": (make_sig_step(1), [4, 2, 6, 3, 6]),
-    "SIG_STEP2": (make_sig_step(2), [4, 2, 6, 3, 6]),
+    "SIG_STEP0": (make_sig_step(0), [4, 2, 6, 3]),
+    "SIG_STEP1": (make_sig_step(1), [4, 2, 6, 3]),
+    "SIG_STEP2": (make_sig_step(2), [4, 2, 6, 3]),
+    "G2_ADDAFF_SEL": (prog_g2_add_aff_sel, [6, 4]),
+    "RUNSUM": (prog_runsum, [6, 6, 6]),
+    "G2X_8A": (make_xmul_run(True, 8, True), [6, 6, 6], {2: 0}),
+    **{f"G2P_{k}": (make_xmul_run(True, k, True), [6, 6, 6]) for k in (1, 2, 4, 8, 16, 32)},
     "G2_PROJ2JAC": (prog_g2_proj_to_jac, [6, 6]),
 }
 for _k, _add in X_RUNS:
@@ -1146,16 +1164,28 @@ def define_instances(progs):
     instance("HC_NORM", "FP2_NORM", [H["H"] + 4, H["N"]], H["S"])
     instance("HC_INVFIN", "FP2_INVFIN", [H["H"] + 4, H["NI"], H["ZI"]], H["S"])
     instance("HC_TOAFF", "G2_TOAFF", [H["H"], H["ZI"], H["XY"]], H["S"])
-    # signature side: sigma | apk | M | R | S | D (subgroup check) | N | NI | XY1 | SJ | scratch
-    G = dict(SIG=0, APK=4, M=6, R=12, S=15, D=21, N=27, NI=28, XY1=29, SJ=31, SC=37)
-    gs = max(sc["SIG_STEP0"], sc["SIG_STEP1"], sc["SIG_STEP2"], sc["G2_SUBCHK"], sc["G1_TOAFF"],
-             sc["G2_PROJ2JAC"])
+    # signature side: sigma | apk | M | R | D (subgroup check) | NI | XY1 | scratch
+    G = dict(SIG=0, APK=4, M=6, R=12, D=15, NI=21, XY1=22, SC=24)
+    gs = max(sc["SIG_STEP0"], sc["SIG_STEP1"], sc["SIG_STEP2"], sc["G2_SUBCHK"], sc["G1_TOAFF"])
     layout("SG", STRIDE=G["SC"] + gs, **G)
     for m in range(3):
-        instance(f"SG_STEP{m}", f"SIG_STEP{m}", [G["SIG"], G["APK"], G["M"], G["R"], G["S"]], G["SC"])
+        instance(f"SG_STEP{m}", f"SIG_STEP{m}", [G["SIG"], G["APK"], G["M"], G["R"]], G["SC"])
     instance("SG_SUBCHK", "G2_SUBCHK", [G["SIG"], G["M"], G["D"]], G["SC"])
     instance("SG_TOAFF", "G1_TOAFF", [G["R"], G["NI"], G["XY1"]], G["SC"])
-    instance("SG_TOJAC", "G2_PROJ2JAC", [G["S"], G["SJ"]], G["SC"])
+    # MSM bucket accumulation: R | Q | scratch
+    layout("MB", R=0, Q=6, S=10, STRIDE=10 + sc["G2_ADDAFF_SEL"])
+    instance("MB_ADD", "G2_ADDAFF_SEL", [0, 6], 10)
+    # MSM trees: pairwise sums out = A + B, and weighted pairs out = A + [2^k] B
+    layout("MT", A=0, B=6, O=12, S=18, STRIDE=18 + max(sc["G2_ADD"], *[sc[f"G2P_{k}"] for k in (1, 2, 4, 8, 16, 32)]))
+    instance("MT_ADD", "G2_ADD", [0, 6, 12], 18)
+    for k in (1, 2, 4, 8, 16, 32):
+        instance(f"MT_P{k}", f"G2P_{k}", [6, 0, 12], 18)  # R = B doubled k times, + base A
+    # final affine conversion: P | N | NI | ZI | XY | scratch
+    layout("MA", P=0, N=6, NI=7, ZI=8, XY=10, S=14,
+           STRIDE=14 + max(sc["FP2_NORM"], sc["FP2_INVFIN"], sc["G2_TOAFF"]))
+    instance("MA_NORM", "FP2_NORM", [4, 6], 14)
+    instance("MA_INVFIN", "FP2_INVFIN", [4, 7, 8], 14)
+    instance("MA_TOAFF", "G2_TOAFF", [0, 8, 10], 14)
 
 
 def compile_all():
