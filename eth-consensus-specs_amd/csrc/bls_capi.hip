@@ -4,6 +4,7 @@
 #include <mutex>
 #include <new>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -18,7 +19,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF,
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT,
   NSLOT
 };
 
@@ -592,7 +593,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     return BLS_E_NOREG;
   }
   G1J* apk;
-  int *status, *flag;
+  int *status, *flag, *mstat;
   G1A *apka, *rP;
   G2A *sig, *H, *saff;
   Fp12 *f, *ft, *fo;
@@ -613,35 +614,41 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_MSMU, msm_scratch_u32(B), msmu);
   SCR(S_MSMF, msm_scratch_fd(), msmf);
   SCR(S_SAFF, 1, saff);
+  SCR(S_MSTAT, B, mstat);
   SCR(S_F, B + 2, f);
   SCR(S_F_T, (B + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
   hipStream_t st = ctx->stream, st2 = ctx->stream2, st3 = ctx->stream3;
+  static const bool serial = getenv("BLS_SERIAL") != nullptr;  // profiling knob: one stream, no overlap
+  if (serial) st2 = st3 = st;
   // stream2: hash_to_G2 of every message, beside the gather / signature branch
   HIPCK(hipEventRecord(ctx->ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, ctx->ev_fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, H, flag));
   HIPCK(hipEventRecord(ctx->ev_join, st2));
   PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
-  PROF(1, launch_sig_decode(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rsc));
-  PROF(10, launch_sig_vm(st, B, status, apka, sig, rsc, rP));
+  PROF(1, launch_sig_decode(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rsc, mstat));
   HIPCK(hipEventRecord(ctx->ev_sig, st));
-  // stream3: S = sum r_i sigma_i and the Miller loop of (-G1, S) -> f[B + 1]
+  // stream3: S = sum r_i sigma_i over the decoded signatures and the Miller
+  // loop of (-G1, S) -> f[B + 1].  It runs beside the subgroup checks: a
+  // decodable signature outside G2 stays in S, so the batch check fails and
+  // fav_finish re-checks every item individually (exact verdicts either way).
   HIPCK(hipStreamWaitEvent(st3, ctx->ev_sig, 0));
   {
     ProfScope ps_(ctx, 11, st3);
-    LK(launch_msm(st3, B, status, rsc, sig, msmu, msmf, saff));
+    LK(launch_msm(st3, B, mstat, rsc, sig, msmu, msmf, saff));
     hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, rP + B);
     LK(hipGetLastError());
     LK(launch_miller_wave(st3, rP + B, saff, nullptr, 1, f + B + 1));
   }
   HIPCK(hipEventRecord(ctx->ev_msm, st3));
+  PROF(10, launch_sig_vm(st, B, status, apka, sig, rsc, rP));
   // stream1: Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-  PROF(5, launch_miller_wave(st, rP, H, status, B, f));
-  PROF(6, launch_fp12_prod_vm(st, f, B, ft, f + B));
+  PROF(5, launch_miller2(st, rP, H, status, B, f));
+  PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
   HIPCK(hipStreamWaitEvent(st, ctx->ev_msm, 0));
   LK(launch_fp12_prod_vm(st, f + B, 2, ft, fo));
   ctx->fav_B = B;

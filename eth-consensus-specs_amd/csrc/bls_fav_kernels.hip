@@ -11,6 +11,8 @@
 #include "bls_lane.h"
 #include "bls_vm.h"
 
+#include <stdlib.h>
+
 namespace bls {
 
 __device__ static const uint8_t DST_POP_FAV[43] = {
@@ -132,7 +134,7 @@ static __device__ uint64_t rlc_scalar_fav(const uint8_t* seed32, uint64_t i, con
 // against the identity key, which the gather already rejected.
 __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
                                                    const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff,
-                                                   G2A* sig, uint64_t* rsc) {
+                                                   G2A* sig, uint64_t* rsc, int* mstat) {
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B) return;
   G1A a{fp_zero(), fp_zero(), true};
@@ -147,6 +149,7 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
   apk_aff[i] = a;
   sig[i] = q;
   status[i] = st;
+  mstat[i] = st;  // decode-time status: the MSM branch starts before the subgroup checks
 }
 
 // (2) the two per-item signature-side chains, 64 steps ([|x|] sigma for the
@@ -217,13 +220,24 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
 }
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+static int env_g(const char* name, int dflt) {
+  const char* v = getenv(name);
+  const int g = v ? atoi(v) : dflt;
+  return (g == 2 || g == 4 || g == 6) ? g : dflt;
+}
 
 hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, G2A* H, int* flag) {
   if (!B) return hipSuccess;
   hipLaunchKernelGGL(k_h2c_sswu, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs32, status, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_h2c_vm<FAV_G>, dim3(nblk(B, FAV_G)), dim3(64), 0, st, B, status, U, H, flag);
+  static const int hg = env_g("BLS_H2C_G", 2);  // tuning knob: items per workgroup
+  if (hg == 4)
+    hipLaunchKernelGGL(k_h2c_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, U, H, flag);
+  else if (hg == 6)
+    hipLaunchKernelGGL(k_h2c_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, U, H, flag);
+  else
+    hipLaunchKernelGGL(k_h2c_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, U, H, flag);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_h2c_fallback, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, flag, H);
@@ -232,17 +246,23 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
 
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
                              const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff, G2A* sig,
-                             uint64_t* rsc) {
+                             uint64_t* rsc, int* mstat) {
   if (!B) return hipSuccess;
   hipLaunchKernelGGL(k_sig_decode, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, sigs96, seed32, apk, status,
-                     apk_aff, sig, rsc);
+                     apk_aff, sig, rsc, mstat);
   return hipGetLastError();
 }
 
 hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const G1A* apk_aff, const G2A* sig,
                          const uint64_t* rsc, G1A* rP) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_vm<FAV_G>, dim3(nblk(B, FAV_G)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
+  static const int sg = env_g("BLS_SIG_G", 4);  // tuning knob: items per workgroup
+  if (sg == 4)
+    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
+  else if (sg == 6)
+    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
+  else
+    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
   return hipGetLastError();
 }
 

@@ -192,35 +192,56 @@ __device__ __forceinline__ void vm_load_terms(uint32_t* w, const uint32_t* src, 
   for (int k = 0; k < VM_MAXT; k++) w[k] = k < n ? src[k] : 0u;
 }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
 // Run program p for G items whose regions start at item0 + g * stride.
 // pred[g]: per-item predicate (sel: bit 0) or table index (lut).  All 64
-// lanes of the workgroup must call it.
+// lanes of the workgroup must call it.  Each pass of a level pads operand
+// lists only to the widest op of that pass (wave max of the per-op widths
+// stored in the destination words), so the term loops are uniform.
 template <int G>
 __device__ __noinline__ void vm_run(const VmProg p, Fd* slots, int item0, int stride, const uint32_t* pred) {
   const int lane = threadIdx.x;
   for (int lv = 0; lv < p.nlevels; lv++) {
     const uint32_t nitems = p.levels[lv][0], na = p.levels[lv][1], nb = p.levels[lv][2], base = p.levels[lv][3];
     const uint32_t total = nitems * G, sw = 1 + na + nb;
-    for (uint32_t k = lane; k < total; k += VM_NT) {
+    const uint32_t npass = (total + VM_NT - 1) / VM_NT;
+    for (uint32_t ps = 0; ps < npass; ps++) {
+      const uint32_t k = (uint32_t)lane + ps * VM_NT;
+      const bool active = k < total;
       const uint32_t j = k / G, g = k % G;
       const int ibase = item0 + (int)g * stride;
       const uint32_t* t = p.terms + base + j * sw;
-      const uint32_t d = t[0];
+      const uint32_t d = active ? t[0] : 0u;
       const uint32_t kind = d >> 30;
+      const uint32_t na_i = (d >> 26) & 15u, nb_i = (d >> 22) & 15u;
+      const bool pick_b = kind == 2u && !(pred[active ? g : 0] & 1u);
+      // uniform operand widths of this pass, per code path
+      const uint32_t wa_mul = wave_max(kind == 1u ? na_i : 0u);
+      const uint32_t wb_mul = wave_max(kind == 1u ? nb_i : 0u);
+      const uint32_t w_lin = wave_max((kind == 0u || kind == 2u) && active ? (pick_b ? nb_i : na_i) : 0u);
+      if (!active) continue;
       uint32_t wa[VM_MAXT];
       Fd out;
       if (kind == 1u) {  // mul
         uint32_t x[14], y[14];
         {
-          vm_load_terms(wa, t + 1, (int)na);
+          vm_load_terms(wa, t + 1, (int)na_i);
           Acc a;
-          vm_lincomb(a, slots, ibase, wa, (int)na);
+          vm_lincomb(a, slots, ibase, wa, (int)wa_mul);
           vm_normalise_fast(x, a);
         }
         {
-          vm_load_terms(wa, t + 1 + na, (int)nb);
+          vm_load_terms(wa, t + 1 + na, (int)nb_i);
           Acc b;
-          vm_lincomb(b, slots, ibase, wa, (int)nb);
+          vm_lincomb(b, slots, ibase, wa, (int)wb_mul);
           vm_normalise_fast(y, b);
         }
         fp_mul_digits_raw(out.d, x, y);
@@ -230,18 +251,16 @@ __device__ __noinline__ void vm_run(const VmProg p, Fd* slots, int item0, int st
         const int stride_t = (int)(w >> 24) - 128;
         out = slots[vm_slot(w, ibase) + (int)pred[g] * stride_t];
       } else {  // lin / sel
-        const bool pick_b = kind == 2u && !(pred[g] & 1u);
         const uint32_t* src = pick_b ? t + 1 + na : t + 1;
-        const int n = pick_b ? (int)nb : (int)na;
-        vm_load_terms(wa, src, n);  // zero-filled past this op's own list
+        vm_load_terms(wa, src, (int)(pick_b ? nb_i : na_i));  // zero-filled past this op's list
         Acc a;
-        vm_lincomb(a, slots, ibase, wa, (int)(na > nb ? na : nb));  // uniform bound
+        vm_lincomb(a, slots, ibase, wa, (int)w_lin);
         vm_normalise(out.d, a);
         vm_reduce(out.d);
       }
       out.d[14] = 0;
       out.d[15] = 0;
-      slots[vm_slot(d & 0x3fffffffu, ibase)] = out;
+      slots[vm_slot(d & 0x3fffffu, ibase)] = out;
     }
     __syncthreads();
   }

@@ -294,3 +294,28 @@ def test_msm_programs_pippenger():
     for p_, r in zip(pts, rs):
         expect = O.g2_add(expect, O.g2_mul(p_, r))
     assert g2_aff(W) == expect
+
+
+@pytest.mark.parametrize("dummy", [False, True])
+def test_shared_accumulator_miller_loop(dummy):
+    """ML2_{FIRST,DBL,ADD}: two pairs share f; a pair with P = (0, 0) only
+    contributes Fp2 factors, which the final exponentiation removes."""
+    P1, Q1 = O.g1_mul(O.G1_GEN, 0x1111), O.g2_mul(O.G2_GEN, 0x2222)
+    P2, Q2 = O.g1_mul(O.G1_GEN, 0x3333), O.g2_mul(O.G2_GEN, 0x4444)
+
+    def pair_frames(P, Q):
+        T = [Q[0][0], Q[0][1], Q[1][0], Q[1][1], 1, 0]
+        Pf = [0, 0] if P is None else [(-P[0]) % O.P, P[1]]
+        return [T, Pf, [Q[0][0], Q[0][1], Q[1][0], Q[1][1]]]
+
+    fr = [[0] * 12] + pair_frames(P1, Q1) + pair_frames(None if dummy else P2, Q2)
+    fr = run(PROGS["ML2_FIRST"], fr)[:7]
+    if (O.X_ABS >> 62) & 1:
+        fr = run(PROGS["ML2_ADD"], fr)[:7]
+    for b in range(61, -1, -1):
+        fr = run(PROGS["ML2_DBL"], fr)[:7]
+        if (O.X_ABS >> b) & 1:
+            fr = run(PROGS["ML2_ADD"], fr)[:7]
+    got = O.final_exponentiation(O.f12_conj(list_f12(fr[0])))
+    expect = O.pairing(P1, Q1) if dummy else O.f12_mul(O.pairing(P1, Q1), O.pairing(P2, Q2))
+    assert got == expect

@@ -597,6 +597,44 @@ def prog_ml_dbl_first(c):
     return {0: line.coeffs(), 1: _t_out(T2)}
 
 
+def make_ml_shared(K, step):
+    """K pairs sharing one Miller accumulator f.  frame 0: f (12); frame
+    1 + 3k, 2 + 3k, 3 + 3k: T_k (6), P_k = (-xP, yP) (2), Q_k (4).
+    step 'dbl':   f <- f^2 * prod_k l_{T_k,T_k}(P_k),  T_k <- 2 T_k
+    step 'first': f <- prod_k l_{T_k,T_k}(P_k)  (f = 1 before)
+    step 'add':   f <- f * prod_k l_{T_k,Q_k}(P_k),   T_k <- T_k + Q_k"""
+
+    def prog(c):
+        f = f12_from_frame(c, 0)
+        outs = {}
+        lines = []
+        for k in range(K):
+            T = (f2_from_frame(c, 1 + 3 * k, 0), f2_from_frame(c, 1 + 3 * k, 2), f2_from_frame(c, 1 + 3 * k, 4))
+            nxP, yP = inp(c, 2 + 3 * k, 0), inp(c, 2 + 3 * k, 1)
+            xQ, yQ = f2_from_frame(c, 3 + 3 * k, 0), f2_from_frame(c, 3 + 3 * k, 2)
+            if step == "add":
+                T2, ln = _ml_line_add(c, T, xQ, yQ, nxP, yP)
+            else:
+                T2, ln = _ml_line_dbl(c, T, nxP, yP)
+            outs[1 + 3 * k] = _t_out(T2)
+            lines.append(ln)
+        if step == "first":
+            z = zero(c)
+            Z2 = F2(z, z)
+            l0, l2, l3 = lines[0]
+            acc = F12(F6(l0, l2, Z2), F6(Z2, l3, Z2))
+            rest = lines[1:]
+        else:
+            acc = f.sqr() if step == "dbl" else f
+            rest = lines
+        for l0, l2, l3 in rest:
+            acc = acc.mul_line(l0, l2, l3)
+        outs[0] = acc.coeffs()
+        return outs
+
+    return prog
+
+
 def prog_ml_add(c):
     """f <- f * l_{T,Q}(P); T <- T + Q."""
     f, T, nxP, yP, xQ, yQ = _pair_frames(c)
@@ -802,6 +840,8 @@ PROGRAMS = {
     "ML_DBL": (prog_ml_dbl, [12, 6, 2, 4]),
     "ML_DBL_FIRST": (prog_ml_dbl_first, [12, 6, 2, 4]),
     "ML_ADD": (prog_ml_add, [12, 6, 2, 4]),
+    **{f"ML{_K}_{_st.upper()}": (make_ml_shared(_K, _st), [12] + [6, 2, 4] * _K)
+       for _K in (2,) for _st in ("dbl", "first", "add")},
     "G2_ADD": (make_pt_add(True), [6, 6, 6]),
     "G1_ADD": (make_pt_add(False), [3, 3, 3]),
     "G1_DAS": (make_dbl_add_sel(False), [3, 2]),
@@ -1027,7 +1067,7 @@ def compile_program(name, builder, frames, alias=None):
 # binding: a program instance places its frames at fixed slot offsets of the
 # item region, so table words carry absolute slot indices.
 #   term word: [31:24] coef + 128 (lut: stride + 128) | [23] const pool | [22:0] slot
-#   dest word: [31:30] kind | [22:0] slot
+#   dest word: [31:30] kind | [29:26] na | [25:22] nb | [21:0] slot
 # --------------------------------------------------------------------------
 LAYOUT = {}      # layout name -> {"stride": n, "consts": {...}} (emitted as C++ constants)
 INSTANCES = []   # (instance name, program name, frame bases, scratch base)
@@ -1064,7 +1104,9 @@ def bind(p, bases, scratch, alias):
     for items in p["levels"]:
         bl = []
         for kind, (fr, ix), a, b in items:
-            d = (KIND[kind] << 30) | slot_of(fr, ix)
+            # dest word: kind | own operand widths (na, nb: 4 bits each) | slot
+            assert slot_of(fr, ix) < (1 << 22)
+            d = (KIND[kind] << 30) | (len(a) << 26) | (len(b) << 22) | slot_of(fr, ix)
             if kind == "lut":
                 (tf, ti, ts), = a
                 ta = [((ts + 128) << 24) | slot_of(tf, ti)]
@@ -1131,6 +1173,11 @@ def define_instances(progs):
     layout("ML", F=0, T=12, P=18, Q=20, S=24, STRIDE=24 + ml_s)
     for nm in ("ML_DBL", "ML_ADD", "ML_DBL_FIRST"):
         instance(nm, nm, [0, 12, 18, 20], 24)
+    # shared-accumulator Miller loop, K = 2 pairs: f | (T, P, Q) x K | scratch
+    m2s = max(sc["ML2_DBL"], sc["ML2_FIRST"], sc["ML2_ADD"])
+    layout("M2", F=0, PAIR=12, PSTRIDE=12, S=36, STRIDE=36 + m2s)
+    for st_ in ("DBL", "FIRST", "ADD"):
+        instance(f"M2_{st_}", f"ML2_{st_}", [0, 12, 18, 20, 24, 30, 32], 36)
     # chunked Fp12 product: acc | in | scratch
     layout("CH", STRIDE=24 + sc["FP12_MUL"])
     instance("CH_MUL", "FP12_MUL", [0, 12, 0], 24)
