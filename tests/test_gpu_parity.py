@@ -217,10 +217,34 @@ def test_fav_batch_adversarial(batch):
     sigs[96 * 3: 96 * 4] = b"\xc0" + bytes(95)               # infinity signature
     sigs[96 * 4: 96 * 5] = bytes(96)                         # undecodable
     sigs[96 * 6 + 92: 96 * 7] = b"\xff" * 4                  # tampered tail
-    expect[[1, 3, 4, 6]] = False
+    q = O.iso_map(O.map_to_curve_sswu((5, 7)))               # on E2, outside G2: decodes, fails the subgroup check
+    assert not O.g2_in_subgroup(q)
+    sigs[96 * 8: 96 * 9] = O.g2_compress(q)
+    expect[[1, 3, 4, 6, 8]] = False
     m = b"".join(msgs[:-1]) + msgs[-1]
     out = batch.fast_aggregate_verify_batch(idx, offs, m, bytes(sigs))
     assert (out == expect).all(), (out, expect)
+
+
+@pytest.mark.parametrize("n_items", [1, 7, 33])
+def test_fav_batch_odd_sizes_all_valid(batch, n_items):
+    """Odd batch sizes exercise the padded pair of the 2-pair Miller groups."""
+    pks, idx, offs, msgs, sigs = _synthetic(128, [3 + (j % 5) for j in range(n_items)], seed=21 + n_items)
+    batch.Registry().load(pks)
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+    assert out.all()
+
+
+def test_fav_batch_only_non_subgroup_signature_invalid(batch):
+    """One decodable non-G2 signature in an otherwise valid batch: the batch
+    check fails and the per-item re-check must flag exactly that item."""
+    pks, idx, offs, msgs, sigs = _synthetic(128, [4] * 9, seed=31)
+    batch.Registry().load(pks)
+    q = O.iso_map(O.map_to_curve_sswu((11, 13)))
+    assert not O.g2_in_subgroup(q)
+    sigs[96 * 4: 96 * 5] = O.g2_compress(q)
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+    assert list(out) == [True] * 4 + [False] + [True] * 4
 
 
 def test_fav_batch_out_of_range_index(batch):
