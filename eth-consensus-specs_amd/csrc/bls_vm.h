@@ -192,13 +192,24 @@ __device__ __forceinline__ void vm_load_terms(uint32_t* w, const uint32_t* src, 
   for (int k = 0; k < VM_MAXT; k++) w[k] = k < n ? src[k] : 0u;
 }
 
+// max over the 64 lanes (all active): DPP within rows of 16, then the four
+// row results by readlane -> a wave-uniform (scalar) value.
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) {
-    const uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64);
-    v = o > v ? o : v;
-  }
-  return v;
+  uint32_t o;
+  o = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v = o > v ? o : v;
+  o = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v = o > v ? o : v;
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+  const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  const uint32_t a = r0 > r1 ? r0 : r1, b = r2 > r3 ? r2 : r3;
+  return a > b ? a : b;
 }
 
 // Run program p for G items whose regions start at item0 + g * stride.
@@ -223,23 +234,28 @@ __device__ __noinline__ void vm_run(const VmProg p, Fd* slots, int item0, int st
       const uint32_t kind = d >> 30;
       const uint32_t na_i = (d >> 26) & 15u, nb_i = (d >> 22) & 15u;
       const bool pick_b = kind == 2u && !(pred[active ? g : 0] & 1u);
-      // uniform operand widths of this pass, per code path
-      const uint32_t wa_mul = wave_max(kind == 1u ? na_i : 0u);
-      const uint32_t wb_mul = wave_max(kind == 1u ? nb_i : 0u);
-      const uint32_t w_lin = wave_max((kind == 0u || kind == 2u) && active ? (pick_b ? nb_i : na_i) : 0u);
+      // uniform operand widths of this pass, per code path: the wave max of
+      // the ops' own widths when several items share the pass (throughput),
+      // the level width for one item (latency: no cross-lane reduction)
+      uint32_t wa_mul = na, wb_mul = nb, w_lin = na > nb ? na : nb;
+      if (G > 1) {
+        wa_mul = wave_max(kind == 1u ? na_i : 0u);
+        wb_mul = wave_max(kind == 1u ? nb_i : 0u);
+        w_lin = wave_max((kind == 0u || kind == 2u) && active ? (pick_b ? nb_i : na_i) : 0u);
+      }
       if (!active) continue;
       uint32_t wa[VM_MAXT];
       Fd out;
-      if (kind == 1u) {  // mul
-        uint32_t x[14], y[14];
+      if (kind == 1u) {  // mul: rows are zero-padded to the level widths, so
+        uint32_t x[14], y[14];  // the loads need no per-op count
         {
-          vm_load_terms(wa, t + 1, (int)na_i);
+          vm_load_terms(wa, t + 1, (int)na);
           Acc a;
           vm_lincomb(a, slots, ibase, wa, (int)wa_mul);
           vm_normalise_fast(x, a);
         }
         {
-          vm_load_terms(wa, t + 1 + na, (int)nb_i);
+          vm_load_terms(wa, t + 1 + na, (int)nb);
           Acc b;
           vm_lincomb(b, slots, ibase, wa, (int)wb_mul);
           vm_normalise_fast(y, b);

@@ -489,6 +489,9 @@ def prog_fp12_sqr(c):
     return {1: a.sqr().coeffs()}
 
 
+CYC_MAT = 1
+
+
 def make_cyc_run(k, mul):
     """frame 0: a, frame 1: base (multiplier), frame 2: out = a^(2^k) [* base]."""
 
@@ -496,7 +499,10 @@ def make_cyc_run(k, mul):
         a = f12_from_frame(c, 0)
         for j in range(k):
             a = a.cyc_sqr()
-            if j + 1 < k or mul:
+            # materialise every CYC_MAT squarings (and before the product):
+            # in between, the next squaring's operands are short linear
+            # forms of the previous products
+            if (j + 1 < k and (j + 1) % CYC_MAT == 0) or (j + 1 == k and mul):
                 a = mat12(a)
         if mul:
             a = a * f12_from_frame(c, 1)
@@ -939,9 +945,12 @@ def compile_program(name, builder, frames, alias=None):
                     items.append((a, 1))
         return dict(items)
 
-    for a in sorted(a for a in need if c.atoms[a][0] in ("prod", "sel")):
-        k, fa, fb = c.atoms[a]
-        c.atoms[a] = (k, shrink(fa), shrink(fb))
+    for a in sorted(a for a in need if c.atoms[a][0] in ("prod", "sel", "lin")):
+        if c.atoms[a][0] == "lin":
+            c.atoms[a] = ("lin", shrink(c.atoms[a][1]))
+        else:
+            k, fa, fb = c.atoms[a]
+            c.atoms[a] = (k, shrink(fa), shrink(fb))
     out_list = [(fr, i, shrink(f)) for fr, i, f in out_list]
 
     level = {}
