@@ -35,7 +35,7 @@ struct bls_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // concurrent branch of the FAV batch (hash_to_G2)
   hipStream_t stream3 = nullptr;  // concurrent branch: sum r_i sigma_i (MSM) + its Miller loop
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sig = nullptr, ev_msm = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sig = nullptr, ev_msm = nullptr, ev_gather = nullptr;
   std::mutex mu;
   std::string err;
   Buf buf[NSLOT];
@@ -231,7 +231,8 @@ int bls_ctx_create(int device, bls_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_sig, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_msm, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_msm, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gather, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return BLS_E_DEVICE;
   }
@@ -258,6 +259,7 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_join);
   (void)hipEventDestroy(ctx->ev_sig);
   (void)hipEventDestroy(ctx->ev_msm);
+  (void)hipEventDestroy(ctx->ev_gather);
   (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream);
@@ -592,9 +594,9 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     ctx->err = "no registry loaded";
     return BLS_E_NOREG;
   }
-  G1J* apk;
-  int *status, *flag, *mstat;
-  G1A *apka, *rP;
+  int *status, *flag, *dstat;
+  G1P* apka;
+  G1A* rP;
   G2A *sig, *H, *saff;
   Fp12 *f, *ft, *fo;
   Fp* U;
@@ -602,7 +604,6 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   uint64_t* rsc;
   uint32_t* msmu;
   uint8_t* d_seed;
-  SCR(S_APK, B, apk);
   SCR(S_STATUS, B + 1, status);
   SCR(S_APKA, B, apka);
   SCR(S_SIG, B, sig);
@@ -614,7 +615,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_MSMU, msm_scratch_u32(B), msmu);
   SCR(S_MSMF, msm_scratch_fd(), msmf);
   SCR(S_SAFF, 1, saff);
-  SCR(S_MSTAT, B, mstat);
+  SCR(S_MSTAT, B, dstat);
   SCR(S_F, B + 2, f);
   SCR(S_F_T, (B + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
@@ -623,29 +624,35 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   hipStream_t st = ctx->stream, st2 = ctx->stream2, st3 = ctx->stream3;
   static const bool serial = getenv("BLS_SERIAL") != nullptr;  // profiling knob: one stream, no overlap
   if (serial) st2 = st3 = st;
-  // stream2: hash_to_G2 of every message, beside the gather / signature branch
+  // Three branches:
+  //   stream1: registry gather (affine apk) -> subgroup / r_i apk_i chains -> Miller loops
+  //   stream2: hash_to_G2 of every message
+  //   stream3: signature decompression + RLC scalars -> MSM S = sum r_i sigma_i
+  //            -> Miller loop of (-G1, S) -> f[B + 1]
   HIPCK(hipEventRecord(ctx->ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, ctx->ev_fork, 0));
+  HIPCK(hipStreamWaitEvent(st3, ctx->ev_fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, H, flag));
   HIPCK(hipEventRecord(ctx->ev_join, st2));
-  PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apk, status));
-  PROF(1, launch_sig_decode(st, B, d_msgs, d_sigs, d_seed, apk, status, apka, sig, rsc, mstat));
-  HIPCK(hipEventRecord(ctx->ev_sig, st));
-  // stream3: S = sum r_i sigma_i over the decoded signatures and the Miller
-  // loop of (-G1, S) -> f[B + 1].  It runs beside the subgroup checks: a
-  // decodable signature outside G2 stays in S, so the batch check fails and
-  // fav_finish re-checks every item individually (exact verdicts either way).
-  HIPCK(hipStreamWaitEvent(st3, ctx->ev_sig, 0));
+  PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
+  HIPCK(hipEventRecord(ctx->ev_sig, st3));
+  PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apka, status));
+  HIPCK(hipEventRecord(ctx->ev_gather, st));
+  // The MSM covers every decoded signature of a valid aggregate key, before
+  // the subgroup checks: a decodable signature outside G2 stays in S, so the
+  // batch check fails and fav_finish re-checks every item individually.
+  HIPCK(hipStreamWaitEvent(st3, ctx->ev_gather, 0));
   {
     ProfScope ps_(ctx, 11, st3);
-    LK(launch_msm(st3, B, mstat, rsc, sig, msmu, msmf, saff));
+    LK(launch_msm(st3, B, status, dstat, rsc, sig, msmu, msmf, saff));
     hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, rP + B);
     LK(hipGetLastError());
     LK(launch_miller_wave(st3, rP + B, saff, nullptr, 1, f + B + 1));
   }
   HIPCK(hipEventRecord(ctx->ev_msm, st3));
-  PROF(10, launch_sig_vm(st, B, status, apka, sig, rsc, rP));
-  // stream1: Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
+  HIPCK(hipStreamWaitEvent(st, ctx->ev_sig, 0));
+  PROF(10, launch_sig_vm(st, B, status, dstat, apka, sig, rsc, rP));
+  // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->ev_join, 0));
   PROF(5, launch_miller2(st, rP, H, status, B, f));
   PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
@@ -667,7 +674,7 @@ static int fav_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   if (batch_ok) {
     PROF(8, launch_status_to_u8(ctx->stream, status, B, d_out));
   } else {
-    PROF(8, launch_fav_single(ctx->stream, B, (G1A*)ctx->buf[S_APKA].p, (G2A*)ctx->buf[S_H].p,
+    PROF(8, launch_fav_single(ctx->stream, B, (G1P*)ctx->buf[S_APKA].p, (G2A*)ctx->buf[S_H].p,
                               (G2A*)ctx->buf[S_SIG].p, status, d_out));
   }
   return 0;

@@ -41,6 +41,10 @@ struct Aff {
   F x, y;
   bool inf;
 };
+// homogeneous projective G1 point (x = X/Z, y = Y/Z; identity (0 : 1 : 0))
+struct G1P {
+  Fp x, y, z;
+};
 typedef Jac<Fp> G1J;
 typedef Jac<Fp2> G2J;
 typedef Aff<Fp> G1A;

@@ -129,35 +129,27 @@ static __device__ uint64_t rlc_scalar_fav(const uint8_t* seed32, uint64_t i, con
   return r ? r : 1;
 }
 
-// (1) lane per item: aggregate key to affine, signature decompression (no
-// subgroup check yet), RLC scalar.  The identity signature can only verify
-// against the identity key, which the gather already rejected.
+// (1) lane per item: signature decompression (no subgroup check yet) and the
+// RLC scalar.  Independent of the registry gather, so it runs beside it.
+// The identity signature can only verify against the identity key, which the
+// gather rejects: it is marked invalid here.
 __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
-                                                   const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff,
-                                                   G2A* sig, uint64_t* rsc, int* mstat) {
+                                                   const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat) {
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B) return;
-  G1A a{fp_zero(), fp_zero(), true};
   G2A q{fp2_zero(), fp2_zero(), true};
-  int st = status[i];
-  if (st) {
-    a = jac_to_aff(apk[i]);
-    if (a.inf) st = 0;
-  }
-  if (st && g2_decompress_lane(q, sigs96 + 96 * i) != DEC_OK) st = 0;
+  const int st = g2_decompress_lane(q, sigs96 + 96 * i) == DEC_OK ? 1 : 0;
   rsc[i] = st ? rlc_scalar_fav(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i) : 0;
-  apk_aff[i] = a;
   sig[i] = q;
-  status[i] = st;
-  mstat[i] = st;  // decode-time status: the MSM branch starts before the subgroup checks
+  dstat[i] = st;
 }
 
 // (2) the two per-item signature-side chains, 64 steps ([|x|] sigma for the
 // subgroup check and r * apk), then the subgroup verdict and r * apk to
 // affine.  sum r_i sigma_i is the batch MSM (bls_msm.hip).
 template <int G>
-__global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G1A* apk_aff, const G2A* sig,
-                                                 const uint64_t* rsc, G1A* rP) {
+__global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const int* dstat, const G1P* apk,
+                                                 const G2A* sig, const uint64_t* rsc, G1A* rP) {
   __shared__ Fd s[WP_NCONST + G * WL_SG_STRIDE];
   __shared__ int live[G];
   __shared__ uint32_t pred[G];
@@ -167,24 +159,24 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const G
   uint64_t r = 0;
   if (lane < G) {
     const size_t i = i0 + lane;
-    live[lane] = i < B && status[i];
+    live[lane] = i < B && status[i] && dstat[i];
     r = live[lane] ? rsc[i] : 0;
   }
   __syncthreads();
   const int item0 = WP_NCONST;
-  // sigma (4) | apk (2) | M = (sigma, 1) (6) | R = (0:1:0) (3)
-  for (int k = lane; k < 15 * G; k += 64) {
-    const int g = k / 15, j = k % 15;
+  // sigma (4) | apk (3, projective) | M = (sigma, 1) (6) | R = (0:1:0) (3)
+  for (int k = lane; k < 16 * G; k += 64) {
+    const int g = k / 16, j = k % 16;
     const size_t i = i0 + g;
     Fp v = fp_zero();
     if (live[g]) {
       const G2A& q = sig[i];
       if (j < 4) v = j == 0 ? q.x.c0 : (j == 1 ? q.x.c1 : (j == 2 ? q.y.c0 : q.y.c1));
-      else if (j < 6) v = j == 4 ? apk_aff[i].x : apk_aff[i].y;
-      else if (j < 10) v = j == 6 ? q.x.c0 : (j == 7 ? q.x.c1 : (j == 8 ? q.y.c0 : q.y.c1));
-      else if (j == 10) v = FP_ONE;
+      else if (j < 7) v = j == 4 ? apk[i].x : (j == 5 ? apk[i].y : apk[i].z);
+      else if (j < 11) v = j == 7 ? q.x.c0 : (j == 8 ? q.x.c1 : (j == 9 ? q.y.c0 : q.y.c1));
+      else if (j == 11) v = FP_ONE;
     }
-    if (j == 13) v = FP_ONE;  // Y of R
+    if (j == 14) v = FP_ONE;  // Y of R
     s[item0 + g * WL_SG_STRIDE + j] = fd_from_fp(v);
   }
   __syncthreads();
@@ -245,24 +237,22 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
 }
 
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
-                             const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff, G2A* sig,
-                             uint64_t* rsc, int* mstat) {
+                             const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_decode, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, sigs96, seed32, apk, status,
-                     apk_aff, sig, rsc, mstat);
+  hipLaunchKernelGGL(k_sig_decode, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, sigs96, seed32, sig, rsc, dstat);
   return hipGetLastError();
 }
 
-hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const G1A* apk_aff, const G2A* sig,
-                         const uint64_t* rsc, G1A* rP) {
+hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff,
+                         const G2A* sig, const uint64_t* rsc, G1A* rP) {
   if (!B) return hipSuccess;
   static const int sg = env_g("BLS_SIG_G", 4);  // tuning knob: items per workgroup
   if (sg == 4)
-    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
+    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rP);
   else if (sg == 6)
-    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
+    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rP);
   else
-    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, apk_aff, sig, rsc, rP);
+    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rP);
   return hipGetLastError();
 }
 

@@ -19,11 +19,11 @@ hipError_t launch_miller(hipStream_t st, const G1A* P, const G2A* Q, const int* 
 hipError_t launch_final_check(hipStream_t st, const Fp12* f, int* out);
 hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n, uint8_t* out, int* ok);
 hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok);
-hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, G1J* apk, int* status);
+hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status);
 hipError_t launch_fav_sig(hipStream_t st, size_t B, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* seed, const G1J* apk, int* status, G1A* apk_aff, G2A* sig, G1A* rP, G2J* rS);
 hipError_t launch_fav_hash(hipStream_t st, size_t B, const uint8_t* msgs, const int* status, G2A* H);
 hipError_t launch_sig_pair(hipStream_t st, const G2J* S, G1A* P, G2A* Q);
-hipError_t launch_fav_single(hipStream_t st, size_t B, const G1A* apk_aff, const G2A* H, const G2A* sig, const int* status, uint8_t* out);
+hipError_t launch_fav_single(hipStream_t st, size_t B, const G1P* apk, const G2A* H, const G2A* sig, const int* status, uint8_t* out);
 hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out);
 hipError_t launch_verify_indexed(hipStream_t st, const uint32_t* idx, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, const uint8_t* msgs, const uint8_t* sigs, uint8_t* out);
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out);
@@ -32,11 +32,11 @@ hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96)
 hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok, uint8_t* out48);
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, G2A* H, int* flag);
-hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff, G2A* sig, uint64_t* rsc, int* mstat);
-hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const G1A* apk_aff, const G2A* sig, const uint64_t* rsc, G1A* rP);
+hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat);
+hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff, const G2A* sig, const uint64_t* rsc, G1A* rP);
 size_t msm_scratch_u32(size_t B);
 size_t msm_scratch_fd();
-hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
+hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
 hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out);

@@ -200,37 +200,81 @@ __global__ void __launch_bounds__(64) k_sk_to_pk_many(const uint8_t* sks32, size
 }
 
 // ------------------------------------------------------- FAV batch path --
-// (1) aggregate pubkeys: one 64-lane workgroup per item, strided mixed
-//     additions from the HBM registry, then an LDS tree.
+// (1) aggregate pubkeys: one 64-lane workgroup per item.  Each lane adds its
+//     strided share of the registry points with the complete projective
+//     mixed addition (Renes-Costello-Batina alg. 8, 11 products, no
+//     exceptional cases), then an LDS tree of complete additions (alg. 7).
+BLS_HD Fp fp_x12(const Fp& a) {  // 3b * a, b = 4
+  const Fp a2 = fp_dbl(a), a4 = fp_dbl(a2);
+  return fp_add(fp_dbl(a4), a4);
+}
+
+__device__ __forceinline__ G1P g1p_add_aff(const G1P& p, const Fp& x2, const Fp& y2) {
+  Fp t0 = fp_mul_v(p.x, x2);
+  Fp t1 = fp_mul_v(p.y, y2);
+  Fp t3 = fp_sub(fp_sub(fp_mul_v(fp_add(x2, y2), fp_add(p.x, p.y)), t0), t1);
+  const Fp t4 = fp_add(fp_mul_v(y2, p.z), p.y);
+  Fp y3 = fp_add(fp_mul_v(x2, p.z), p.x);
+  t0 = fp_add(fp_dbl(t0), t0);
+  const Fp t2 = fp_x12(p.z);
+  Fp z3 = fp_add(t1, t2);
+  t1 = fp_sub(t1, t2);
+  y3 = fp_x12(y3);
+  G1P r;
+  r.x = fp_sub(fp_mul_v(t3, t1), fp_mul_v(t4, y3));
+  r.y = fp_add(fp_mul_v(t1, z3), fp_mul_v(y3, t0));
+  r.z = fp_add(fp_mul_v(z3, t4), fp_mul_v(t0, t3));
+  return r;
+}
+
+__device__ __forceinline__ G1P g1p_add(const G1P& p, const G1P& q) {
+  Fp t0 = fp_mul_v(p.x, q.x);
+  Fp t1 = fp_mul_v(p.y, q.y);
+  Fp t2 = fp_mul_v(p.z, q.z);
+  const Fp t3 = fp_sub(fp_sub(fp_mul_v(fp_add(p.x, p.y), fp_add(q.x, q.y)), t0), t1);
+  const Fp t4 = fp_sub(fp_sub(fp_mul_v(fp_add(p.y, p.z), fp_add(q.y, q.z)), t1), t2);
+  Fp y3 = fp_sub(fp_sub(fp_mul_v(fp_add(p.x, p.z), fp_add(q.x, q.z)), t0), t2);
+  t0 = fp_add(fp_dbl(t0), t0);
+  t2 = fp_x12(t2);
+  Fp z3 = fp_add(t1, t2);
+  t1 = fp_sub(t1, t2);
+  y3 = fp_x12(y3);
+  G1P r;
+  r.x = fp_sub(fp_mul_v(t3, t1), fp_mul_v(t4, y3));
+  r.y = fp_add(fp_mul_v(t1, z3), fp_mul_v(y3, t0));
+  r.z = fp_add(fp_mul_v(z3, t4), fp_mul_v(t0, t3));
+  return r;
+}
+
 __global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
-                                                   const uint8_t* reg_ok, uint32_t reg_n, G1J* apk, int* status) {
-  __shared__ G1J sh[64];
+                                                   const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status) {
+  __shared__ G1P sh[64];
   __shared__ int bad;
   const size_t b = blockIdx.x;
   if (b >= B) return;
   if (threadIdx.x == 0) bad = 0;
   __syncthreads();
   const uint64_t lo = offs[b], hi = offs[b + 1];
-  G1J acc = jac_identity<Fp>();
+  G1P acc{fp_zero(), FP_ONE, fp_zero()};  // identity (0 : 1 : 0)
   int mybad = 0;
   for (uint64_t j = lo + threadIdx.x; j < hi; j += 64) {
-    uint32_t k = idx[j];
+    const uint32_t k = idx[j];
     if (k >= reg_n || !reg_ok[k]) {
       mybad = 1;
     } else {
-      acc = jac_add_aff(acc, reg[k]);
+      acc = g1p_add_aff(acc, reg[k].x, reg[k].y);
     }
   }
   if (mybad) atomicOr(&bad, 1);
   sh[threadIdx.x] = acc;
   __syncthreads();
   for (int s = 32; s > 0; s >>= 1) {
-    if (threadIdx.x < s) sh[threadIdx.x] = jac_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    if ((int)threadIdx.x < s) sh[threadIdx.x] = g1p_add(sh[threadIdx.x], sh[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // projective aggregate key; the identity is invalid (KeyValidate of the sum)
     apk[b] = sh[0];
-    status[b] = (hi > lo && !bad) ? 1 : 0;
+    status[b] = (hi > lo && !bad && !fp_is_zero(sh[0].z)) ? 1 : 0;
   }
 }
 
@@ -297,7 +341,7 @@ __global__ void k_sig_pair(const G2J* S, G1A* P, G2A* Q) {
 }
 
 // (4) fallback: individual checks e(apk_i, H_i) e(-G1, sig_i) == 1
-__global__ void __launch_bounds__(64) k_fav_single(size_t B, const G1A* apk_aff, const G2A* H, const G2A* sig,
+__global__ void __launch_bounds__(64) k_fav_single(size_t B, const G1P* apk, const G2A* H, const G2A* sig,
                                                    const int* status, uint8_t* out) {
   size_t i = gtid();
   if (i >= B) return;
@@ -307,7 +351,9 @@ __global__ void __launch_bounds__(64) k_fav_single(size_t B, const G1A* apk_aff,
   }
   G1A g = g1_generator();
   g.y = fp_neg(g.y);
-  out[i] = pairing_check2(apk_aff[i], H[i], g, sig[i]) ? 1 : 0;
+  const Fp zi = fp_inv(apk[i].z);
+  const G1A a{fp_mul(apk[i].x, zi), fp_mul(apk[i].y, zi), false};
+  out[i] = pairing_check2(a, H[i], g, sig[i]) ? 1 : 0;
 }
 
 __global__ void k_status_to_u8(const int* status, size_t B, uint8_t* out) {
@@ -485,7 +531,7 @@ hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, ui
   return hipSuccess;
 }
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
-                             const uint8_t* reg_ok, uint32_t reg_n, G1J* apk, int* status) {
+                             const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status) {
   if (!B) return hipSuccess;
   LAUNCH(k_fav_gather, (unsigned)B, 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
   return hipSuccess;
@@ -505,10 +551,10 @@ hipError_t launch_sig_pair(hipStream_t st, const G2J* S, G1A* P, G2A* Q) {
   LAUNCH(k_sig_pair, 1, 64, st, S, P, Q);
   return hipSuccess;
 }
-hipError_t launch_fav_single(hipStream_t st, size_t B, const G1A* apk_aff, const G2A* H, const G2A* sig,
+hipError_t launch_fav_single(hipStream_t st, size_t B, const G1P* apk, const G2A* H, const G2A* sig,
                              const int* status, uint8_t* out) {
   if (!B) return hipSuccess;
-  LAUNCH(k_fav_single, nblk(B, 64), 64, st, B, apk_aff, H, sig, status, out);
+  LAUNCH(k_fav_single, nblk(B, 64), 64, st, B, apk, H, sig, status, out);
   return hipSuccess;
 }
 hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out) {

@@ -50,6 +50,14 @@ BLS_HD Fp fp_pow_w3(const Fp& a, const uint32_t* e, int nbits) {
   return r;
 }
 
+// a^(p-2): inversion with uniform control flow (no divergent GCD loop)
+BLS_HD Fp fp_inv_fermat_w3(const Fp& a) { return fp_pow_w3(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
+
+BLS_HD Fp2 fp2_inv_lane(const Fp2& a) {
+  const Fp ni = fp_inv_fermat_w3(fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1)));
+  return Fp2{fp_mul_i(a.c0, ni), fp_neg(fp_mul_i(a.c1, ni))};
+}
+
 BLS_HD Fp fp_sqrt_cand(const Fp& a) { return fp_pow_w3(a, EXP_SQRT, EXP_SQRT_BITS); }      // a^((p+1)/4)
 BLS_HD Fp fp_pow_pm3_4(const Fp& a) { return fp_pow_w3(a, EXP_SQRT_M3, EXP_SQRT_M3_BITS); }  // a^((p-3)/4)
 
@@ -95,7 +103,11 @@ BLS_HDNI void map_to_curve_sswu_lane(Fp2& x, Fp2& y, const Fp2& u) {
   const Fp2 u2 = fp2_sqr(u);
   const Fp2 zu2 = fp2_mul(SSWU_Z, u2);
   const Fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+#ifndef BLS_SSWU_GCD
+  const Fp2 x1 = fp2_is_zero(den) ? SSWU_B_OVER_ZA : fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv_lane(den)));
+#else
   const Fp2 x1 = fp2_is_zero(den) ? SSWU_B_OVER_ZA : fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv(den)));
+#endif
   const Fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
   const Fp nrm1 = fp_add(fp_sqr_i(gx1.c0), fp_sqr_i(gx1.c1));
   const Fp c = fp_sqrt_cand(nrm1);

@@ -20,12 +20,13 @@ constexpr int MSM_W = 8, MSM_NB = MSM_W * 256;
 constexpr int MSM_G = 4;  // buckets per workgroup
 
 // cnt[MSM_NB] must be zero on entry.
-__global__ void __launch_bounds__(256) k_msm_count(size_t B, const int* status, const uint64_t* rsc, uint32_t* cnt) {
+__global__ void __launch_bounds__(256) k_msm_count(size_t B, const int* status, const int* status2, const uint64_t* rsc,
+                                                   uint32_t* cnt) {
   const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= B * MSM_W) return;
   const size_t i = k / MSM_W;
   const int w = (int)(k % MSM_W);
-  if (!status[i]) return;
+  if (!status[i] || !status2[i]) return;
   const uint32_t d = (uint32_t)(rsc[i] >> (8 * w)) & 0xffu;
   if (d) atomicAdd(&cnt[w * 256 + d], 1u);
 }
@@ -42,13 +43,13 @@ __global__ void k_msm_scan(const uint32_t* cnt, uint32_t* off, uint32_t* cur) {
   off[MSM_NB] = s;
 }
 
-__global__ void __launch_bounds__(256) k_msm_scatter(size_t B, const int* status, const uint64_t* rsc, uint32_t* cur,
-                                                     uint32_t* lst) {
+__global__ void __launch_bounds__(256) k_msm_scatter(size_t B, const int* status, const int* status2,
+                                                     const uint64_t* rsc, uint32_t* cur, uint32_t* lst) {
   const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= B * MSM_W) return;
   const size_t i = k / MSM_W;
   const int w = (int)(k % MSM_W);
-  if (!status[i]) return;
+  if (!status[i] || !status2[i]) return;
   const uint32_t d = (uint32_t)(rsc[i] >> (8 * w)) & 0xffu;
   if (d) lst[atomicAdd(&cur[w * 256 + d], 1u)] = (uint32_t)i;
 }
@@ -168,8 +169,8 @@ __global__ void __launch_bounds__(64) k_msm_affine(const Fd* pt, G2A* out) {
 size_t msm_scratch_u32(size_t B) { return (size_t)3 * MSM_NB + 1 + MSM_W * B; }
 size_t msm_scratch_fd() { return (size_t)MSM_NB * 6 + 64 * 128 * 6 + 64 * 64 * 6; }
 
-hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const uint64_t* rsc, const G2A* sig,
-                      uint32_t* scr, Fd* pts, G2A* out) {
+hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc,
+                      const G2A* sig, uint32_t* scr, Fd* pts, G2A* out) {
   uint32_t* cnt = scr;
   uint32_t* off = cnt + MSM_NB;
   uint32_t* cur = off + MSM_NB + 1;
@@ -181,13 +182,13 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const uint64_
   if (e != hipSuccess) return e;
   const unsigned nb = (unsigned)((B * MSM_W + 255) / 256);
   if (B) {
-    hipLaunchKernelGGL(k_msm_count, dim3(nb), dim3(256), 0, st, B, status, rsc, cnt);
+    hipLaunchKernelGGL(k_msm_count, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(64), 0, st, cnt, off, cur);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (B) {
-    hipLaunchKernelGGL(k_msm_scatter, dim3(nb), dim3(256), 0, st, B, status, rsc, cur, lst);
+    hipLaunchKernelGGL(k_msm_scatter, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cur, lst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k_msm_bucket<MSM_G>, dim3(MSM_NB / MSM_G), dim3(64), 0, st, off, lst, sig, bsum);

@@ -255,7 +255,7 @@ def test_signature_step_programs():
     sig = O.g2_mul(O.G2_GEN, 0x1234_5678_9ABC)
     apk = O.g1_mul(O.G1_GEN, 0xDEADBEEF)
     r = rng.getrandbits(64) | (1 << 63)
-    fr = [[sig[0][0], sig[0][1], sig[1][0], sig[1][1]], [apk[0], apk[1]],
+    fr = [[sig[0][0], sig[0][1], sig[1][0], sig[1][1]], g1_proj(apk),
           [sig[0][0], sig[0][1], sig[1][0], sig[1][1], 1, 0], g1_proj(None)]
     for b in range(63, -1, -1):
         mode = 0 if b == 63 else (2 if (O.X_ABS >> b) & 1 else 1)

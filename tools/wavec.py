@@ -786,7 +786,7 @@ def prog_fp2_inv_finish(c):
 
 def make_sig_step(mode):
     """One bit step of the two per-item signature-side chains of an FAV item:
-      frame 0: sigma affine (x, y)          frame 1: apk affine (x, y)
+      frame 0: sigma affine (x, y)          frame 1: apk projective (X : Y : Z)
       frame 2: M (projective, [|x|] sigma chain)
       frame 3: R (G1 projective, r * apk)
     R <- pred ? 2R + apk : 2R (pred = bit of the item's RLC scalar);
@@ -795,7 +795,7 @@ def make_sig_step(mode):
 
     def prog(c):
         sig = (f2_from_frame(c, 0, 0), f2_from_frame(c, 0, 2))
-        apk = (inp(c, 1, 0), inp(c, 1, 1))
+        apk = pt_from_frame(c, 1, 0, False)  # projective: no inversion after the gather
         out = {}
         if mode:
             M = rcb_dbl(pt_from_frame(c, 2, 0, True), B2_3)
@@ -804,7 +804,7 @@ def make_sig_step(mode):
             out[2] = pt_out(M)
         R = pt_from_frame(c, 3, 0, False)
         D = rcb_dbl(R, B1_3)
-        A = rcb_add_aff(D, apk, B1_3)
+        A = rcb_add(D, apk, B1_3)
         out[3] = [sel(c, a, d) for a, d in zip(pt_out(A), pt_out(D))]
         return out
 
@@ -860,9 +860,9 @@ PROGRAMS = {
     "G1_TOAFF": (prog_proj_to_aff1, [3, 1, 2]),
     "FP2_NORM": (prog_fp2_norm, [2, 1]),
     "FP2_INVFIN": (prog_fp2_inv_finish, [2, 1, 2]),
-    "SIG_STEP0": (make_sig_step(0), [4, 2, 6, 3]),
-    "SIG_STEP1": (make_sig_step(1), [4, 2, 6, 3]),
-    "SIG_STEP2": (make_sig_step(2), [4, 2, 6, 3]),
+    "SIG_STEP0": (make_sig_step(0), [4, 3, 6, 3]),
+    "SIG_STEP1": (make_sig_step(1), [4, 3, 6, 3]),
+    "SIG_STEP2": (make_sig_step(2), [4, 3, 6, 3]),
     "G2_ADDAFF_SEL": (prog_g2_add_aff_sel, [6, 4]),
     "RUNSUM": (prog_runsum, [6, 6, 6]),
     "G2X_8A": (make_xmul_run(True, 8, True), [6, 6, 6], {2: 0}),
@@ -1221,7 +1221,7 @@ def define_instances(progs):
     instance("HC_INVFIN", "FP2_INVFIN", [H["H"] + 4, H["NI"], H["ZI"]], H["S"])
     instance("HC_TOAFF", "G2_TOAFF", [H["H"], H["ZI"], H["XY"]], H["S"])
     # signature side: sigma | apk | M | R | D (subgroup check) | NI | XY1 | scratch
-    G = dict(SIG=0, APK=4, M=6, R=12, D=15, NI=21, XY1=22, SC=24)
+    G = dict(SIG=0, APK=4, M=7, R=13, D=16, NI=22, XY1=23, SC=25)
     gs = max(sc["SIG_STEP0"], sc["SIG_STEP1"], sc["SIG_STEP2"], sc["G2_SUBCHK"], sc["G1_TOAFF"])
     layout("SG", STRIDE=G["SC"] + gs, **G)
     for m in range(3):
