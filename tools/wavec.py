@@ -890,7 +890,7 @@ def _pool_index(v):
     return CONST_POOL[v]
 
 
-def compile_program(name, builder, frames, alias=None):
+def compile_program(name, builder, frames, alias=None, schedule="asap"):
     alias = alias or {}
 
     def canon(key):
@@ -966,6 +966,24 @@ def compile_program(name, builder, frames, alias=None):
     work = [a for a in need if c.atoms[a][0] in ("prod", "lin", "sel", "lut")]
     for a in work:
         lvl(a)
+    if schedule == "alap":
+        # as late as possible (within the ASAP depth): an op moves to one level
+        # before its earliest consumer, so values live shorter (fewer LDS slots)
+        depth_ = max([level[a] for a in work] or [0])
+        users = defaultdict(list)
+        for a in work:
+            for s_ in deps(a):
+                users[s_].append(a)
+        out_of = defaultdict(list)
+        for fr, i, f in out_list:
+            for s_ in f:
+                out_of[s_].append((fr, i))
+        for a in sorted(work, key=lambda a: -level[a]):
+            lim = depth_ if out_of.get(a) else depth_ + 1
+            if users.get(a):
+                lim = min(lim, min(level[u] for u in users[a]) - 1)
+            if lim > level[a]:
+                level[a] = lim
     # last level at which each input slot is read
     last_read = defaultdict(int)
     for a in work:
@@ -1246,7 +1264,13 @@ def define_instances(progs):
 
 def compile_all():
     CONST_POOL.clear()
-    progs = [compile_program(n, *spec) for n, spec in PROGRAMS.items()]
+    progs = []
+    for n, spec in PROGRAMS.items():
+        # as-soon-as-possible vs as-late-as-possible levelling: keep whichever
+        # needs fewer scratch slots (shorter item stride, more items per LDS)
+        a = compile_program(n, *spec, schedule="asap")
+        b = compile_program(n, *spec, schedule="alap")
+        progs.append(b if b["frames"][-1] < a["frames"][-1] else a)
     define_instances(progs)
     return progs
 
