@@ -60,6 +60,7 @@ _SIGS = {
     "bls_partials_check": (_ip, [_vp, _u8p, _sz]),
     "bls_fav_batch_finish_dev": (_ip, [_vp, _ip, _vp]),
     "bls_registry_generate": (_ip, [_vp, ctypes.c_uint64, _sz, _vp]),
+    "bls_last_fallback_stats": (_ip, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "bls_profile_enable": (_ip, [_vp, _ip]),
     "bls_profile_read": (_ip, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), _ip]),
     "bls_profile_name": (ctypes.c_char_p, [_ip]),

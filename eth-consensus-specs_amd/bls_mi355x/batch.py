@@ -87,6 +87,14 @@ def verify_batch(indices: np.ndarray, msgs32, sigs96, ctx=None) -> np.ndarray:
     return out.astype(bool)
 
 
+def fallback_stats(ctx=None) -> tuple[int, int]:
+    """(batched final-exponentiation checks, bisection rounds) of the last batch call; (0, 0) if it passed."""
+    c = ctx or _native.context()
+    checks, rounds = ctypes.c_uint64(), ctypes.c_uint64()
+    c.check(c.lib.bls_last_fallback_stats(c.h, ctypes.byref(checks), ctypes.byref(rounds)))
+    return int(checks.value), int(rounds.value)
+
+
 def sign_batch(sks32, msgs32, ctx=None) -> bytes:
     c = ctx or _native.context()
     sk, m = _u8(sks32), _u8(msgs32)

@@ -20,6 +20,8 @@ enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
   S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT,
+  // bisection fallback (fav_bisect)
+  S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
   NSLOT
 };
 
@@ -46,6 +48,8 @@ struct bls_ctx {
   // last prepared FAV batch
   size_t fav_B = 0;
   bool fav_ready = false;
+  // last bisection fallback: batched final-exponentiation checks and rounds
+  uint64_t bis_checks = 0, bis_rounds = 0;
   // per-kernel hipEvent timing of the FAV path (bls_profile_*)
   bool prof_on = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -664,7 +668,85 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   return 0;
 }
 
-static int fav_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
+// Bisection fallback ("a failing batch falls back to
+// per-signature bisection").  Per-item Miller values f_i of the pairs
+// (r_i apk_i, H_i), (-r_i G1, sigma_i) form the leaves of a 16-ary product
+// tree; each round final-exponentiates, in one batched launch, the children of
+// the nodes that failed the round before.  A leaf that fails is an invalid
+// item; every item under a passing node keeps its per-item status.  With k bad
+// items among B this costs about 16 k log16(B / k) checks in log16(B) rounds
+// instead of B checks.  root_bad: the caller already knows the product fails.
+static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
+  const size_t B = ctx->fav_B;
+  const int* status = (const int*)ctx->buf[S_STATUS].p;
+  const uint64_t* rsc = (const uint64_t*)ctx->buf[S_RSC].p;
+  const G1A* rP = (const G1A*)ctx->buf[S_RP].p;
+  const G2A* H = (const G2A*)ctx->buf[S_H].p;
+  const G2A* sig = (const G2A*)ctx->buf[S_SIG].p;
+  std::vector<size_t> off{0}, cnt{B};
+  while (cnt.back() > 1) {
+    off.push_back(off.back() + cnt.back());
+    cnt.push_back((cnt.back() + 15) / 16);
+  }
+  const size_t total = off.back() + cnt.back();
+  G1A* P2;
+  G2A* Q2;
+  int *st2, *d_res;
+  Fp12* tree;
+  uint32_t* d_sel;
+  uint8_t* d_bad;
+  SCR(S_BP, 2 * B, P2);
+  SCR(S_BQ, 2 * B, Q2);
+  SCR(S_BS, 2 * B, st2);
+  SCR(S_BT, total, tree);
+  SCR(S_BSEL, B + 16, d_sel);
+  SCR(S_BRES, B + 16, d_res);
+  SCR(S_BBAD, B, d_bad);
+  hipStream_t st = ctx->stream;
+  LK(launch_bisect_pairs(st, B, rsc, status, rP, H, sig, P2, Q2, st2));
+  LK(launch_miller2(st, P2, Q2, st2, 2 * B, tree));
+  for (size_t L = 0; L + 1 < cnt.size(); L++)
+    LK(launch_fp12_chunk_prod(st, tree + off[L], cnt[L], 16, tree + off[L + 1]));
+  std::vector<uint8_t> bad(B, 0);
+  std::vector<uint32_t> cand, sel;
+  std::vector<int> res;
+  int L = (int)cnt.size() - 1;
+  cand.push_back(0);
+  ctx->bis_checks = ctx->bis_rounds = 0;
+  auto children = [&](int lvl, uint32_t node, std::vector<uint32_t>& next) {
+    for (size_t c = (size_t)node * 16; c < (size_t)node * 16 + 16 && c < cnt[lvl - 1]; c++) next.push_back((uint32_t)c);
+  };
+  if (root_bad && L > 0) {  // skip re-checking the root
+    std::vector<uint32_t> next;
+    children(L, 0, next);
+    cand.swap(next);
+    L--;
+  }
+  for (; L >= 0 && !cand.empty(); L--) {
+    const size_t n = cand.size();
+    sel.resize(n);
+    for (size_t k = 0; k < n; k++) sel[k] = (uint32_t)(off[L] + cand[k]);
+    CK(h2d(ctx, d_sel, sel.data(), 4 * n));
+    PROF(8, launch_final_check_sel(st, tree, d_sel, n, d_res));
+    res.resize(n);
+    CK(d2h(ctx, res.data(), d_res, 4 * n));
+    ctx->bis_checks += n;
+    ctx->bis_rounds += 1;
+    std::vector<uint32_t> next;
+    for (size_t k = 0; k < n; k++) {
+      if (res[k]) continue;
+      if (L == 0) bad[cand[k]] = 1;
+      else children(L, cand[k], next);
+    }
+    cand.swap(next);
+  }
+  CK(h2d(ctx, d_bad, bad.data(), B));
+  LK(launch_verdicts(st, status, d_bad, B, d_out));
+  HIPCK(hipStreamSynchronize(st));  // `bad` is pageable host memory
+  return 0;
+}
+
+static int fav_finish(bls_ctx* ctx, int batch_ok, bool root_bad, uint8_t* d_out) {
   if (!ctx->fav_ready) {
     ctx->err = "no prepared FAV batch";
     return BLS_E_ARG;
@@ -672,12 +754,11 @@ static int fav_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   size_t B = ctx->fav_B;
   int* status = (int*)ctx->buf[S_STATUS].p;
   if (batch_ok) {
+    ctx->bis_checks = ctx->bis_rounds = 0;
     PROF(8, launch_status_to_u8(ctx->stream, status, B, d_out));
-  } else {
-    PROF(8, launch_fav_single(ctx->stream, B, (G1P*)ctx->buf[S_APKA].p, (G2A*)ctx->buf[S_H].p,
-                              (G2A*)ctx->buf[S_SIG].p, status, d_out));
+    return 0;
   }
-  return 0;
+  return fav_bisect(ctx, root_bad, d_out);
 }
 
 static void host_seed(uint8_t seed[32]) {
@@ -688,13 +769,12 @@ static void host_seed(uint8_t seed[32]) {
   for (size_t i = got; i < 32; i++) seed[i] = (uint8_t)(i * 131 + 7);
 }
 
-int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* offsets, size_t B, const uint8_t* msgs32,
+// One host-buffer FAV batch: copies in, RLC batch check, bisection on failure.
+static int fav_batch_host(bls_ctx* ctx, const uint32_t* idx, const uint64_t* offsets, size_t B, const uint8_t* msgs32,
                           const uint8_t* sigs96, uint8_t* out) {
-  API_ENTER(ctx);
-  if ((!offsets || !msgs32 || !sigs96 || !out) && B) return BLS_E_ARG;
-  if (!B) return 1;
   const uint64_t nidx = offsets[B];
   if (nidx && !idx) return BLS_E_ARG;
+  if (nidx > 0xffffffffull * 64) return BLS_E_ARG;
   for (size_t b = 0; b < B; b++)
     if (offsets[b + 1] < offsets[b]) return BLS_E_ARG;
   uint32_t* d_idx;
@@ -715,32 +795,37 @@ int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* off
   CK(fav_prepare(ctx, d_idx, d_offs, B, d_m, d_s, seed, &f));
   int ok = run_final_check(ctx, f);
   if (ok < 0) return ok;
-  CK(fav_finish(ctx, ok, d_out));
+  CK(fav_finish(ctx, ok, true, d_out));
   CK(d2h(ctx, out, d_out, B));
   return 1;
 }
 
+int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* offsets, size_t B, const uint8_t* msgs32,
+                          const uint8_t* sigs96, uint8_t* out) {
+  API_ENTER(ctx);
+  if ((!offsets || !msgs32 || !sigs96 || !out) && B) return BLS_E_ARG;
+  if (!B) return 1;
+  return fav_batch_host(ctx, idx, offsets, B, msgs32, sigs96, out);
+}
+
+// Gossip firehose: B independent Verify calls with
+// registry keys = B FastAggregateVerify calls of one key each, through the
+// same RLC batch (one final exponentiation) and bisection path.
 int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
                              uint8_t* out) {
   API_ENTER(ctx);
   if ((!idx || !msgs32 || !sigs96 || !out) && B) return BLS_E_ARG;
   if (!B) return 1;
-  if (!ctx->reg || !ctx->reg_n) {
-    ctx->err = "no registry loaded";
-    return BLS_E_NOREG;
-  }
-  uint32_t* d_idx;
-  uint8_t *d_m, *d_s, *d_out;
-  SCR(S_IN0, B, d_idx);
-  SCR(S_IN1, 32 * B, d_m);
-  SCR(S_IN2, 96 * B, d_s);
-  SCR(S_IN3, B, d_out);
-  CK(h2d(ctx, d_idx, idx, B * 4));
-  CK(h2d(ctx, d_m, msgs32, 32 * B));
-  CK(h2d(ctx, d_s, sigs96, 96 * B));
-  LK(launch_verify_indexed(ctx->stream, d_idx, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, d_m, d_s, d_out));
-  CK(d2h(ctx, out, d_out, B));
-  return 1;
+  std::vector<uint64_t> offs(B + 1);
+  for (size_t i = 0; i <= B; i++) offs[i] = i;
+  return fav_batch_host(ctx, idx, offs.data(), B, msgs32, sigs96, out);
+}
+
+int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds) {
+  API_ENTER(ctx);
+  if (fe_checks) *fe_checks = ctx->bis_checks;
+  if (rounds) *rounds = ctx->bis_rounds;
+  return 0;
 }
 
 // ------------------------------------------------------ device-resident --
@@ -808,7 +893,7 @@ int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
 int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   API_ENTER(ctx);
   if (!d_out) return BLS_E_ARG;
-  CK(fav_finish(ctx, batch_ok, d_out));
+  CK(fav_finish(ctx, batch_ok, false, d_out));
   HIPCK(hipStreamSynchronize(ctx->stream));
   return 1;
 }

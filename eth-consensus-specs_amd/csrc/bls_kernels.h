@@ -8,24 +8,17 @@ hipError_t launch_key_validate(hipStream_t st, const uint8_t* pks, size_t n, G1A
 hipError_t launch_sig_validate(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
 hipError_t launch_g1_sum_aff(hipStream_t st, const G1A* in, const int* ok, size_t n, G1J* tmp, G1J* out);
 hipError_t launch_g2_sum_aff(hipStream_t st, const G2A* in, const int* ok, size_t n, G2J* tmp, G2J* out);
-hipError_t launch_g2_sum_jac(hipStream_t st, const G2J* in, size_t n, G2J* tmp, G2J* out);
-hipError_t launch_fp12_prod(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out);
 hipError_t launch_g1_compress(hipStream_t st, const G1J* in, uint8_t* out48, int* is_inf);
 hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96);
 hipError_t launch_verify_single(hipStream_t st, const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig, int* out);
 hipError_t launch_verify_apk(hipStream_t st, const G1J* apk, const uint8_t* msg, uint32_t len, const uint8_t* sig, int* out);
 hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst, uint32_t dst_len, G2A* out);
-hipError_t launch_miller(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
-hipError_t launch_final_check(hipStream_t st, const Fp12* f, int* out);
 hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n, uint8_t* out, int* ok);
 hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok);
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status);
-hipError_t launch_fav_sig(hipStream_t st, size_t B, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* seed, const G1J* apk, int* status, G1A* apk_aff, G2A* sig, G1A* rP, G2J* rS);
-hipError_t launch_fav_hash(hipStream_t st, size_t B, const uint8_t* msgs, const int* status, G2A* H);
-hipError_t launch_sig_pair(hipStream_t st, const G2J* S, G1A* P, G2A* Q);
-hipError_t launch_fav_single(hipStream_t st, size_t B, const G1P* apk, const G2A* H, const G2A* sig, const int* status, uint8_t* out);
+hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP, const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2);
+hipError_t launch_verdicts(hipStream_t st, const int* status, const uint8_t* bad, size_t B, uint8_t* out);
 hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out);
-hipError_t launch_verify_indexed(hipStream_t st, const uint32_t* idx, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, const uint8_t* msgs, const uint8_t* sigs, uint8_t* out);
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out);
 hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, Fp12* f);
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96);
@@ -39,6 +32,9 @@ size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
+// nsel independent checks: out[b] = (FE(f[sel[b]]) == 1)
+hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out);
+hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out);
 hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out);
 
 }  // namespace bls

@@ -81,19 +81,6 @@ __global__ void __launch_bounds__(64) k_g2_sum_aff(const G2A* in, const int* ok,
   if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
 }
 
-__global__ void __launch_bounds__(64) k_fp12_prod(const Fp12* in, size_t n, Fp12* out) {
-  __shared__ Fp12 sh[64];
-  Fp12 acc = fp12_one();
-  for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < n; i += (size_t)gridDim.x * 64) acc = fp12_mul(acc, in[i]);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 32; s > 0; s >>= 1) {
-    if (threadIdx.x < s) sh[threadIdx.x] = fp12_mul(sh[threadIdx.x], sh[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
-}
-
 // ------------------------------------------------------------- encoding --
 __global__ void k_g1_compress(const G1J* in, uint8_t* out48, int* is_inf) {
   if (threadIdx.x || blockIdx.x) return;
@@ -137,17 +124,6 @@ __global__ void __launch_bounds__(64) k_hash_many(const uint8_t* msgs, const uin
   const uint8_t* d = dst ? dst : DST_POP_DEV;
   uint32_t dl = dst ? dst_len : 43;
   out[i] = jac_to_aff(hash_to_g2(msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), d, dl));
-}
-
-__global__ void __launch_bounds__(64) k_miller(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
-  size_t i = gtid();
-  if (i >= n) return;
-  f[i] = (!ok || ok[i]) ? miller_loop(P[i], Q[i]) : fp12_one();
-}
-
-__global__ void k_final_check(const Fp12* f, int* out) {
-  if (threadIdx.x || blockIdx.x) return;
-  *out = fp12_is_one(final_exponentiation(f[0])) ? 1 : 0;
 }
 
 __global__ void k_g2_compress_aff(const G2A* in, uint8_t* out96) {
@@ -278,101 +254,40 @@ __global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const ui
   }
 }
 
-// RLC scalar r_i = first 8 bytes of SHA-256(seed || i || msg || sig), nonzero.
-static __device__ uint64_t rlc_scalar(const uint8_t* seed32, uint64_t i, const uint8_t* msg32, const uint8_t* sig96) {
-  Sha256 s;
-  sha256_init(s);
-  sha256_update(s, seed32, 32);
-  for (int k = 0; k < 8; k++) sha256_byte(s, (uint8_t)(i >> (8 * k)));
-  sha256_update(s, msg32, 32);
-  sha256_update(s, sig96, 96);
-  uint8_t d[32];
-  sha256_final(s, d);
-  uint64_t r = 0;
-  for (int k = 0; k < 8; k++) r = (r << 8) | d[k];
-  return r ? r : 1;
-}
-
-// (2a) per item: signature decode + subgroup check, apk affine, RLC scalars.
-__global__ void __launch_bounds__(64) k_fav_sig(size_t B, const uint8_t* msgs32, const uint8_t* sigs96,
-                                                const uint8_t* seed32, const G1J* apk, int* status, G1A* apk_aff,
-                                                G2A* sig, G1A* rP, G2J* rS) {
+// (4) bisection fallback (fav_bisect in bls_capi.hip).  Per item i the two
+//     pairs (r_i apk_i, H_i) and (-r_i G1, sigma_i): the product of their
+//     Miller values over any subset is that subset's random-linear-combination
+//     check, with the same r_i as the whole-batch check (e(-r_i G1, sigma_i) =
+//     e(-G1, r_i sigma_i)).  This kernel computes -r_i G1 and lays the pairs
+//     out for k_miller2_vm (2 pairs per accumulator -> one Fp12 per item).
+__global__ void __launch_bounds__(64) k_bisect_pairs(size_t B, const uint64_t* rsc, const int* status, const G1A* rP,
+                                                     const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2) {
   size_t i = gtid();
   if (i >= B) return;
-  G1A a{fp_zero(), fp_zero(), true};
-  G2A s{fp2_zero(), fp2_zero(), true};
-  int st = status[i];
+  const int st = status[i];
+  G1A ng{fp_zero(), fp_zero(), true};
   if (st) {
-    a = jac_to_aff(apk[i]);
-    if (a.inf) st = 0;
+    G1A g = g1_generator();
+    g.y = fp_neg(g.y);
+    ng = jac_to_aff(jac_mul_u64(jac_from_aff(g), rsc[i]));
   }
-  if (st && !sig_validate(s, sigs96 + 96 * i)) st = 0;
-  if (st) {
-    uint64_t r = rlc_scalar(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i);
-    rP[i] = jac_to_aff(jac_mul_u64(jac_from_aff(a), r));
-    rS[i] = jac_mul_u64(jac_from_aff(s), r);
-  } else {
-    rP[i] = G1A{fp_zero(), fp_zero(), true};
-    rS[i] = jac_identity<Fp2>();
-  }
-  apk_aff[i] = a;
-  sig[i] = s;
-  status[i] = st;
+  P2[2 * i] = rP[i];
+  P2[2 * i + 1] = ng;
+  Q2[2 * i] = H[i];
+  Q2[2 * i + 1] = sig[i];
+  st2[2 * i] = st;
+  st2[2 * i + 1] = st;
 }
 
-// (2b) per item: hash_to_G2 of the 32-byte signing root.
-__global__ void __launch_bounds__(64) k_fav_hash(size_t B, const uint8_t* msgs32, const int* status, G2A* H) {
+// Verdicts: valid iff the per-item checks passed and bisection did not isolate it.
+__global__ void k_verdicts(const int* status, const uint8_t* bad, size_t B, uint8_t* out) {
   size_t i = gtid();
-  if (i >= B) return;
-  if (status && !status[i]) {
-    H[i] = G2A{fp2_zero(), fp2_zero(), true};
-    return;
-  }
-  H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_DEV, 43));
-}
-
-// Affine conversion of the summed signature side, negated generator pair.
-__global__ void k_sig_pair(const G2J* S, G1A* P, G2A* Q) {
-  if (threadIdx.x || blockIdx.x) return;
-  *Q = jac_to_aff(S[0]);
-  G1A g = g1_generator();
-  g.y = fp_neg(g.y);
-  *P = g;
-}
-
-// (4) fallback: individual checks e(apk_i, H_i) e(-G1, sig_i) == 1
-__global__ void __launch_bounds__(64) k_fav_single(size_t B, const G1P* apk, const G2A* H, const G2A* sig,
-                                                   const int* status, uint8_t* out) {
-  size_t i = gtid();
-  if (i >= B) return;
-  if (!status[i]) {
-    out[i] = 0;
-    return;
-  }
-  G1A g = g1_generator();
-  g.y = fp_neg(g.y);
-  const Fp zi = fp_inv(apk[i].z);
-  const G1A a{fp_mul(apk[i].x, zi), fp_mul(apk[i].y, zi), false};
-  out[i] = pairing_check2(a, H[i], g, sig[i]) ? 1 : 0;
+  if (i < B) out[i] = (status[i] && !bad[i]) ? 1 : 0;
 }
 
 __global__ void k_status_to_u8(const int* status, size_t B, uint8_t* out) {
   size_t i = gtid();
   if (i < B) out[i] = status[i] ? 1 : 0;
-}
-
-// Gossip: registry-indexed single Verify per lane (no batching across items).
-__global__ void __launch_bounds__(64) k_verify_indexed(const uint32_t* idx, size_t B, const G1A* reg,
-                                                       const uint8_t* reg_ok, uint32_t reg_n, const uint8_t* msgs32,
-                                                       const uint8_t* sigs96, uint8_t* out) {
-  size_t i = gtid();
-  if (i >= B) return;
-  uint32_t k = idx[i];
-  if (k >= reg_n || !reg_ok[k]) {
-    out[i] = 0;
-    return;
-  }
-  out[i] = core_verify_point(reg[k], msgs32 + 32 * i, 32, DST_POP_DEV, 43, sigs96 + 96 * i) ? 1 : 0;
 }
 
 // Fp12 <-> 576 big-endian bytes (w-basis order c0..c5, each Fp2 as c0||c1)
@@ -470,22 +385,6 @@ hipError_t launch_g2_sum_aff(hipStream_t st, const G2A* in, const int* ok, size_
   LAUNCH((k_jac_sum<Fp2, 64>), 1, 64, st, tmp, (size_t)g, out);
   return hipSuccess;
 }
-hipError_t launch_g2_sum_jac(hipStream_t st, const G2J* in, size_t n, G2J* tmp, G2J* out) {
-  unsigned g = nblk(n, 64);
-  if (g > 1024) g = 1024;
-  if (g == 0) g = 1;
-  LAUNCH((k_jac_sum<Fp2, 64>), g, 64, st, in, n, tmp);
-  LAUNCH((k_jac_sum<Fp2, 64>), 1, 64, st, tmp, (size_t)g, out);
-  return hipSuccess;
-}
-hipError_t launch_fp12_prod(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out) {
-  unsigned g = nblk(n, 64);
-  if (g > 512) g = 512;
-  if (g == 0) g = 1;
-  LAUNCH(k_fp12_prod, g, 64, st, in, n, tmp);
-  LAUNCH(k_fp12_prod, 1, 64, st, tmp, (size_t)g, out);
-  return hipSuccess;
-}
 hipError_t launch_g1_compress(hipStream_t st, const G1J* in, uint8_t* out48, int* is_inf) {
   LAUNCH(k_g1_compress, 1, 64, st, in, out48, is_inf);
   return hipSuccess;
@@ -510,15 +409,6 @@ hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t*
   LAUNCH(k_hash_many, nblk(n, 64), 64, st, msgs, offs, n, dst, dst_len, out);
   return hipSuccess;
 }
-hipError_t launch_miller(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
-  if (!n) return hipSuccess;
-  LAUNCH(k_miller, nblk(n, 64), 64, st, P, Q, ok, n, f);
-  return hipSuccess;
-}
-hipError_t launch_final_check(hipStream_t st, const Fp12* f, int* out) {
-  LAUNCH(k_final_check, 1, 64, st, f, out);
-  return hipSuccess;
-}
 hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n,
                             uint8_t* out, int* ok) {
   if (!n) return hipSuccess;
@@ -536,36 +426,20 @@ hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t
   LAUNCH(k_fav_gather, (unsigned)B, 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
   return hipSuccess;
 }
-hipError_t launch_fav_sig(hipStream_t st, size_t B, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* seed,
-                          const G1J* apk, int* status, G1A* apk_aff, G2A* sig, G1A* rP, G2J* rS) {
+hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP,
+                               const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2) {
   if (!B) return hipSuccess;
-  LAUNCH(k_fav_sig, nblk(B, 64), 64, st, B, msgs, sigs, seed, apk, status, apk_aff, sig, rP, rS);
+  LAUNCH(k_bisect_pairs, nblk(B, 64), 64, st, B, rsc, status, rP, H, sig, P2, Q2, st2);
   return hipSuccess;
 }
-hipError_t launch_fav_hash(hipStream_t st, size_t B, const uint8_t* msgs, const int* status, G2A* H) {
+hipError_t launch_verdicts(hipStream_t st, const int* status, const uint8_t* bad, size_t B, uint8_t* out) {
   if (!B) return hipSuccess;
-  LAUNCH(k_fav_hash, nblk(B, 64), 64, st, B, msgs, status, H);
-  return hipSuccess;
-}
-hipError_t launch_sig_pair(hipStream_t st, const G2J* S, G1A* P, G2A* Q) {
-  LAUNCH(k_sig_pair, 1, 64, st, S, P, Q);
-  return hipSuccess;
-}
-hipError_t launch_fav_single(hipStream_t st, size_t B, const G1P* apk, const G2A* H, const G2A* sig,
-                             const int* status, uint8_t* out) {
-  if (!B) return hipSuccess;
-  LAUNCH(k_fav_single, nblk(B, 64), 64, st, B, apk, H, sig, status, out);
+  LAUNCH(k_verdicts, nblk(B, 256), 256, st, status, bad, B, out);
   return hipSuccess;
 }
 hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out) {
   if (!B) return hipSuccess;
   LAUNCH(k_status_to_u8, nblk(B, 256), 256, st, status, B, out);
-  return hipSuccess;
-}
-hipError_t launch_verify_indexed(hipStream_t st, const uint32_t* idx, size_t B, const G1A* reg, const uint8_t* reg_ok,
-                                 uint32_t reg_n, const uint8_t* msgs, const uint8_t* sigs, uint8_t* out) {
-  if (!B) return hipSuccess;
-  LAUNCH(k_verify_indexed, nblk(B, 64), 64, st, idx, B, reg, reg_ok, reg_n, msgs, sigs, out);
   return hipSuccess;
 }
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out) {

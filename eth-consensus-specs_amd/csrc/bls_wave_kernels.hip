@@ -161,14 +161,20 @@ __device__ void fe_pow_x(Fd* s) {
 }
 
 // Product of n Fp12 values, then the final exponentiation; *out = (result == 1).
+// With sel != nullptr, workgroup b checks the single value fin[sel[b]] and
+// writes out[b] (the batched checks of a bisection round).
 // Easy part (p^6-1)(p^2+1); hard part via (x-1)^2 (x+p) (x^2+p^2-1) + 3, which
 // returns e^3 (e == 1 <=> e^3 == 1 since gcd(3, r) = 1).
-__global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, int* out) {
+__global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, const uint32_t* sel, int* out) {
   __shared__ Fd s[WP_NCONST + WL_FE_STRIDE];
   __shared__ Fp12 inv;
   __shared__ int okc;
   const int lane = threadIdx.x;
   vm_load_consts(s);
+  if (sel) {
+    fin += sel[blockIdx.x];
+    out += blockIdx.x;
+  }
   load_fp12(fe_reg(s, 0), fin);
   for (int i = 1; i < n; i++) {
     load_fp12(fe_reg(s, 1), fin + i);
@@ -265,7 +271,19 @@ hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int*
 }
 
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out) {
-  hipLaunchKernelGGL(k_final_check_vm, dim3(1), dim3(64), 0, st, f, n, out);
+  hipLaunchKernelGGL(k_final_check_vm, dim3(1), dim3(64), 0, st, f, n, (const uint32_t*)nullptr, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out) {
+  if (!nsel) return hipSuccess;
+  hipLaunchKernelGGL(k_final_check_vm, dim3((unsigned)nsel), dim3(64), 0, st, f, 1, sel, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_chunk_prod, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, in, n, chunk, out);
   return hipGetLastError();
 }
 

@@ -91,14 +91,22 @@ size_t bls_registry_size(bls_ctx* ctx);
 /* B FastAggregateVerify calls over registry indices: item b uses
  * idx[offsets[b] .. offsets[b+1]) (offsets has B+1 entries), message
  * msgs32[32 b ..], signature sigs96[96 b ..].  out[b] = 1/0.  One random-
- * linear-combination pairing check for the whole batch, per-item fallback
- * on failure.  Returns 1 or BLS_E_*. */
+ * linear-combination pairing check for the whole batch; on failure a
+ * bisection (16-ary product tree, batched final exponentiations) isolates the
+ * invalid items.  Returns 1 or BLS_E_*. */
 int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* offsets, size_t B, const uint8_t* msgs32,
                           const uint8_t* sigs96, uint8_t* out);
 
-/* B independent Verify calls with registry indices (gossip firehose). */
+/* B independent Verify calls with registry indices (gossip firehose): the
+ * same RLC batch check + bisection as bls_fav_batch_indexed with one key per
+ * item.  Returns 1 or BLS_E_*. */
 int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const uint8_t* msgs32,
                              const uint8_t* sigs96, uint8_t* out);
+
+/* Fallback statistics of the last batch call on this context: the number of
+ * batched final-exponentiation checks and bisection rounds it ran (both 0
+ * when the whole-batch check passed).  Returns 0 or BLS_E_*. */
+int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds);
 
 /* Synthetic registry for benchmarks: pk_i = (first_sk + i) * G1 written
  * straight into the HBM registry (all valid); compressed keys are copied
@@ -127,7 +135,8 @@ int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_
 int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n);
 /* Phase 2: write verdicts for the batch prepared by the last
  * bls_fav_batch_partial_dev call on this context.  batch_ok = result of
- * bls_partials_check; when 0 every item is re-checked individually. */
+ * bls_partials_check; when 0 this shard is bisected (its own product is
+ * re-checked first, so a bad shard elsewhere leaves these verdicts intact). */
 int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out);
 
 /* ---- tracing: hipEvent time per kernel of the FAV path ------------------ */

@@ -1,0 +1,167 @@
+"""GPU parity of the batch configs of SURVEY.md §8(d): adversarial FAV
+batches (C5, bisection fallback), gossip Verify batches (C4), epoch-shaped FAV
+batches (C3) and AggregateVerify with many distinct messages (C5), checked
+against verdicts known by construction and the C oracle (oracle/bls_oracle.c).
+Requires an MI355X."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import bls_oracle as O
+from oracle import bls_oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+
+N_REG = 1 << 14
+G1_INF = b"\xc0" + bytes(47)
+BAD_PK_0x40 = b"\x40" + bytes(47)
+
+
+@pytest.fixture(scope="module")
+def batch():
+    from bls_mi355x import batch as b
+    return b
+
+
+@pytest.fixture(scope="module")
+def registry(batch):
+    """Registry sk_i = i + 1 (N_REG keys) with two invalid entries: G1 infinity
+    at index 1 and a 0x40-flag encoding at index 2."""
+    reg = batch.Registry()
+    pks = bytearray(reg.generate(N_REG, first_sk=1, want_bytes=True))
+    pks[48:96] = G1_INF
+    pks[96:144] = BAD_PK_0x40
+    valid = reg.load(bytes(pks))
+    assert not valid[1] and not valid[2] and valid.sum() == N_REG - 2
+    return bytes(pks)
+
+
+def _make_batch(batch, B, n, seed, bad_pk_items=()):
+    """B committees of n distinct valid registry keys (>= 3); item j signs
+    SHA256(seed||j) with the sum of its secret keys."""
+    rng = np.random.default_rng(seed)
+    idx = np.stack([rng.choice(np.arange(3, N_REG), size=n, replace=False) for _ in range(B)]).astype(np.uint32)
+    for j, k in bad_pk_items:
+        idx[j, 0] = k
+    offs = np.arange(B + 1, dtype=np.uint64) * n
+    msgs = [hashlib.sha256(seed.to_bytes(8, "little") + j.to_bytes(8, "little")).digest() for j in range(B)]
+    agg = [int(a) % O.R for a in (idx.astype(np.int64) + 1).sum(axis=1)]
+    sigs = bytearray(batch.sign_batch(b"".join(int(a).to_bytes(32, "big") for a in agg), b"".join(msgs)))
+    return idx.reshape(-1), offs, msgs, sigs
+
+
+def _corrupt(sigs, msgs, j, kind, B):
+    if kind == "wrong_msg":  # a valid G2 point for another message: only the pairing check catches it
+        k = (j + 1) % B
+        sigs[96 * j: 96 * j + 96] = sigs[96 * k: 96 * k + 96]
+    elif kind == "inf_sig":
+        sigs[96 * j: 96 * j + 96] = b"\xc0" + bytes(95)
+    elif kind == "zero_sig":
+        sigs[96 * j: 96 * j + 96] = bytes(96)
+    elif kind == "ff_tail":
+        sigs[96 * j + 92: 96 * j + 96] = b"\xff" * 4
+    else:
+        raise AssertionError(kind)
+
+
+KINDS = ["wrong_msg", "inf_sig", "zero_sig", "ff_tail", "g1_inf_pk", "pk_0x40"]
+
+
+@pytest.mark.parametrize("k", [1, 8, 64])
+def test_adversarial_fav_batch_bisection(batch, registry, k):
+    """1024 FAV (n = 64) with k bad entries of every SURVEY §8(d) C5 kind at
+    seeded positions; bisection must isolate exactly those items."""
+    B, n = 1024, 64
+    rng = np.random.default_rng(100 + k)
+    bad = sorted(rng.choice(B, size=k, replace=False).tolist())
+    kinds = {j: KINDS[t % len(KINDS)] for t, j in enumerate(bad)}
+    pk_bad = [(j, 1 if kinds[j] == "g1_inf_pk" else 2) for j in bad if kinds[j] in ("g1_inf_pk", "pk_0x40")]
+    idx, offs, msgs, sigs = _make_batch(batch, B, n, seed=200 + k, bad_pk_items=pk_bad)
+    for j in bad:
+        if kinds[j] not in ("g1_inf_pk", "pk_0x40"):
+            _corrupt(sigs, msgs, j, kinds[j], B)
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+    expect = np.ones(B, dtype=bool)
+    expect[bad] = False
+    assert (out == expect).all(), np.nonzero(out != expect)
+    checks, rounds = batch.fallback_stats()
+    n_wrong = sum(1 for j in bad if kinds[j] == "wrong_msg")
+    assert n_wrong > 0 and rounds >= 2  # a valid-point forgery forces the bisection
+    assert checks < B                    # ... which costs fewer checks than one per item
+    # C oracle on a few items (a bad one and a good one), through the compressed keys
+    good = next(j for j in range(B) if j not in bad)
+    for j in (bad[0], good):
+        pkl = [registry[48 * int(x): 48 * int(x) + 48] for x in idx[n * j: n * j + n]]
+        assert OC.FastAggregateVerify(pkl, msgs[j], bytes(sigs[96 * j: 96 * j + 96])) == bool(expect[j])
+
+
+def test_fav_batch_all_valid_has_no_fallback(batch, registry):
+    idx, offs, msgs, sigs = _make_batch(batch, 300, 16, seed=5)
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+    assert out.all()
+    assert batch.fallback_stats() == (0, 0)
+
+
+def test_fav_batch_every_item_bad(batch, registry):
+    """Worst case for bisection: every item is a wrong-message forgery."""
+    B = 40
+    idx, offs, msgs, sigs = _make_batch(batch, B, 8, seed=6)
+    rolled = sigs[96:] + sigs[:96]
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(rolled))
+    assert not out.any()
+
+
+def test_epoch_shaped_fav_batch(batch, registry):
+    """C3 shape at reduced size: a seeded permutation of the registry split into
+    slots x committees, one distinct message per (slot, committee)."""
+    slots, per_slot, n = 8, 16, 96
+    perm = np.random.default_rng(77).permutation(np.arange(3, N_REG))[: slots * per_slot * n].astype(np.uint32)
+    B = slots * per_slot
+    offs = np.arange(B + 1, dtype=np.uint64) * n
+    msgs = [hashlib.sha256(b"epoch" + j.to_bytes(4, "little")).digest() for j in range(B)]
+    agg = [int(a) % O.R for a in (perm.reshape(B, n).astype(np.int64) + 1).sum(axis=1)]
+    sigs = batch.sign_batch(b"".join(int(a).to_bytes(32, "big") for a in agg), b"".join(msgs))
+    out = batch.fast_aggregate_verify_batch(perm, offs, b"".join(msgs), sigs)
+    assert out.all()
+
+
+def test_gossip_verify_batch(batch, registry):
+    """C4 at reduced size: B single-key Verify calls against the registry."""
+    B = 2000
+    rng = np.random.default_rng(9)
+    idx = rng.integers(3, N_REG, size=B).astype(np.uint32)
+    idx[17] = 1  # G1-infinity registry entry
+    msgs = [hashlib.sha256(b"gossip" + j.to_bytes(4, "little")).digest() for j in range(B)]
+    sigs = bytearray(batch.sign_batch(b"".join(int(k + 1).to_bytes(32, "big") for k in idx), b"".join(msgs)))
+    sigs[96 * 5: 96 * 6] = sigs[96 * 6: 96 * 7]
+    sigs[96 * 1500: 96 * 1501] = b"\xc0" + bytes(95)
+    out = batch.verify_batch(idx, b"".join(msgs), bytes(sigs))
+    expect = np.ones(B, dtype=bool)
+    expect[[5, 17, 1500]] = False
+    assert (out == expect).all(), np.nonzero(out != expect)
+    for j in (5, 6, 17):
+        pk = registry[48 * int(idx[j]): 48 * int(idx[j]) + 48]
+        assert OC.Verify(pk, msgs[j], bytes(sigs[96 * j: 96 * j + 96])) == bool(expect[j])
+
+
+@pytest.mark.parametrize("N", [128, 1024])
+def test_aggregate_verify_many_messages(N):
+    """C5: AggregateVerify with N distinct messages through the drop-in API."""
+    from bls_mi355x import batch as b
+    from bls_mi355x import bls as shim
+
+    shim.use_mi355x()
+    shim.bls_active = True
+    sks = [(7919 * (i + 1)) % O.R for i in range(N)]
+    pks = b.sk_to_pk_batch(b"".join(k.to_bytes(32, "big") for k in sks))
+    pkl = [pks[48 * i: 48 * i + 48] for i in range(N)]
+    msgs = [hashlib.sha256(b"av" + i.to_bytes(4, "little")).digest() for i in range(N)]
+    sigs = b.sign_batch(b"".join(k.to_bytes(32, "big") for k in sks), b"".join(msgs))
+    agg = shim.Aggregate([sigs[96 * i: 96 * i + 96] for i in range(N)])
+    assert agg == OC.Aggregate([sigs[96 * i: 96 * i + 96] for i in range(N)])
+    assert shim.AggregateVerify(pkl, msgs, agg) is True
+    swapped = msgs[:]
+    swapped[0], swapped[1] = swapped[1], swapped[0]
+    assert shim.AggregateVerify(pkl, swapped, agg) is False
+    assert OC.AggregateVerify(pkl[:128], msgs[:128], agg) is (N == 128)
