@@ -149,6 +149,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight (no overlap of passes)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel hipEvent timing")
     args = ap.parse_args()
 
@@ -189,6 +190,15 @@ def main():
 
     from bls_mi355x.dist import allgather_partials
 
+    exchange = (lambda p: allgather_partials(p, device=f"cuda:{local}")) if dist is not None else None
+
+    def passes(k: int) -> list:
+        """k passes over the batch; by default pass j+1 is submitted before pass j is final-exponentiated
+        (two batches in flight, bls_fav_job_*), so every pass completes inside the call."""
+        if args.no_pipeline:
+            return [step(os.urandom(32)) for _ in range(k)]
+        return rb.run_pipelined([os.urandom(32) for _ in range(k)], exchange)
+
     def step(seed32: bytes) -> bool:
         part = rb.partial(seed32)
         if dist is not None:
@@ -197,8 +207,8 @@ def main():
         rb.finish(ok)
         return ok
 
-    for w in range(args.warmup):
-        assert step(os.urandom(32)), "warmup batch failed the pairing check"
+    if args.warmup:
+        assert all(passes(args.warmup)), "warmup batch failed the pairing check"
     v = rb.verdicts()
     assert v.all(), f"{(~v).sum()} valid aggregates rejected"
 
@@ -207,7 +217,7 @@ def main():
         prof.start()
     barrier_sync()
     t0 = time.perf_counter()
-    oks = [step(os.urandom(32)) for _ in range(args.steps)]
+    oks = passes(args.steps)
     barrier_sync()
     dt = time.perf_counter() - t0
     kern = prof.read() if not args.no_profile else {}

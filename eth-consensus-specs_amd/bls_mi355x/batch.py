@@ -17,6 +17,8 @@ import numpy as np
 
 from . import _native
 
+FAV_JOBS = 2  # BLS_FAV_JOBS in include/blsmi355x.h: batches in flight on one context
+
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
@@ -154,7 +156,9 @@ class ResidentFavBatch:
         self.B = int(np.asarray(offsets).size - 1)
         self.msgs = DeviceBuffer(self.ctx, _u8(msgs32))
         self.sigs = DeviceBuffer(self.ctx, _u8(sigs96))
-        self.out = DeviceBuffer(self.ctx, nbytes=self.B)
+        self.outs = [DeviceBuffer(self.ctx, nbytes=self.B) for _ in range(FAV_JOBS)]
+        self.out = self.outs[0]
+        self.last_job = 0
 
     def partial(self, seed32: bytes | None = None) -> bytes:
         seed = seed32 if seed32 is not None else os.urandom(32)
@@ -172,9 +176,51 @@ class ResidentFavBatch:
     def finish(self, batch_ok: bool) -> None:
         c = self.ctx
         c.check(c.lib.bls_fav_batch_finish_dev(c.h, 1 if batch_ok else 0, self.out.ptr))
+        self.last_job = 0
+
+    # ---- pipelined passes (bls_fav_job_*): up to FAV_JOBS batches in flight --
+    def submit(self, job: int, seed32: bytes) -> None:
+        c = self.ctx
+        c.check(c.lib.bls_fav_job_submit_dev(c.h, job, self.idx.ptr, self.offs.ptr, self.B, self.msgs.ptr,
+                                             self.sigs.ptr, seed32))
+
+    def job_partial(self, job: int) -> bytes:
+        buf = ctypes.create_string_buffer(576)
+        c = self.ctx
+        c.check(c.lib.bls_fav_job_partial(c.h, job, buf))
+        return buf.raw
+
+    def job_check(self, job: int, partials: bytes) -> bool:
+        c = self.ctx
+        return c.check(c.lib.bls_fav_job_check(c.h, job, partials, len(partials) // 576)) == 1
+
+    def job_finish(self, job: int, batch_ok: bool) -> None:
+        c = self.ctx
+        c.check(c.lib.bls_fav_job_finish_dev(c.h, job, 1 if batch_ok else 0, self.outs[job].ptr))
+        self.last_job = job
+
+    def run_pipelined(self, seeds, exchange=None) -> list:
+        """One pass over the batch per seed, pass k+1 submitted before pass k is
+        final-exponentiated (its front kernels overlap pass k's tail).
+        exchange(partial) -> concatenated partials of all ranks (multi-GPU
+        all-gather); every pass is complete (verdicts written) on return."""
+        seeds = list(seeds)
+        oks = []
+        if not seeds:
+            return oks
+        self.submit(0, seeds[0])
+        for k in range(len(seeds)):
+            job = k % FAV_JOBS
+            if k + 1 < len(seeds):
+                self.submit((k + 1) % FAV_JOBS, seeds[k + 1])
+            part = self.job_partial(job)
+            ok = self.job_check(job, exchange(part) if exchange else part)
+            self.job_finish(job, ok)
+            oks.append(ok)
+        return oks
 
     def verdicts(self) -> np.ndarray:
-        return self.out.to_host().astype(bool)
+        return self.outs[self.last_job].to_host().astype(bool)
 
     def run(self) -> np.ndarray:
         ok = self.check_partials(self.partial())
@@ -182,7 +228,7 @@ class ResidentFavBatch:
         return self.verdicts()
 
     def free(self):
-        for b in (self.idx, self.offs, self.msgs, self.sigs, self.out):
+        for b in (self.idx, self.offs, self.msgs, self.sigs, *self.outs):
             b.free()
 
 

@@ -32,24 +32,37 @@ struct Buf {
 
 }  // namespace
 
-struct bls_ctx {
-  int device = 0;
+// Per-batch device state, streams and events.  A context owns
+// BLS_FAV_JOBS of them so that consecutive FAV batches can be in flight
+// together (bls_fav_job_*): batch k+1's front kernels fill the GPU while
+// batch k's Miller product is final-exponentiated.  The per-call API and the
+// registry use job 0.
+struct Job {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // concurrent branch of the FAV batch (hash_to_G2)
   hipStream_t stream3 = nullptr;  // concurrent branch: sum r_i sigma_i (MSM) + its Miller loop
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sig = nullptr, ev_msm = nullptr, ev_gather = nullptr;
+  hipEvent_t ev_partial = nullptr;  // the batch's 576-byte partial is in h_partial
+  uint8_t* h_partial = nullptr;     // pinned host copy of the partial
+  Buf buf[NSLOT];
+  // last prepared FAV batch
+  size_t fav_B = 0;
+  bool fav_ready = false;
+  bool partial_pending = false;
+  // last bisection fallback: batched final-exponentiation checks and rounds
+  uint64_t bis_checks = 0, bis_rounds = 0;
+};
+
+struct bls_ctx {
+  int device = 0;
+  Job jobs[BLS_FAV_JOBS];
+  Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
   std::string err;
-  Buf buf[NSLOT];
   // registry (HBM resident)
   G1A* reg = nullptr;
   uint8_t* reg_ok = nullptr;
   size_t reg_n = 0;
-  // last prepared FAV batch
-  size_t fav_B = 0;
-  bool fav_ready = false;
-  // last bisection fallback: batched final-exponentiation checks and rounds
-  uint64_t bis_checks = 0, bis_rounds = 0;
   // per-kernel hipEvent timing of the FAV path (bls_profile_*)
   bool prof_on = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -83,10 +96,10 @@ template <class T>
 int scratch(bls_ctx* ctx, int s, size_t count, T** out) {
   size_t bytes = count * sizeof(T);
   if (bytes == 0) bytes = 16;
-  Buf& b = ctx->buf[s];
+  Buf& b = ctx->j->buf[s];
   if (b.cap < bytes) {
     if (b.p) {
-      HIPCK(hipStreamSynchronize(ctx->stream));
+      HIPCK(hipStreamSynchronize(ctx->j->stream));
       HIPCK(hipFree(b.p));
       b.p = nullptr;
       b.cap = 0;
@@ -106,12 +119,12 @@ int scratch(bls_ctx* ctx, int s, size_t count, T** out) {
   } while (0)
 
 int h2d(bls_ctx* ctx, void* d, const void* h, size_t n) {
-  if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, ctx->stream));
+  if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, ctx->j->stream));
   return 0;
 }
 int d2h(bls_ctx* ctx, void* h, const void* d, size_t n) {
-  if (n) HIPCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  if (n) HIPCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->j->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   return 0;
 }
 
@@ -135,7 +148,7 @@ int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** o
   SCR(S_G1A, n + 1, d_a);
   SCR(S_OK, n + 1, d_ok);
   CK(h2d(ctx, d_in, pks, 48 * n));
-  LK(launch_key_validate(ctx->stream, d_in, n, d_a, d_ok));
+  LK(launch_key_validate(ctx->j->stream, d_in, n, d_a, d_ok));
   std::vector<int> ok(n);
   CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
   *outA = d_a;
@@ -151,7 +164,7 @@ struct ProfScope {
   int id;
   hipStream_t st;
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  ProfScope(bls_ctx* c_, int id_, hipStream_t st_ = nullptr) : c(c_), id(id_), st(st_ ? st_ : c_->stream) {
+  ProfScope(bls_ctx* c_, int id_, hipStream_t st_ = nullptr) : c(c_), id(id_), st(st_ ? st_ : c_->j->stream) {
     if (!c->prof_on) return;
     if (c->prof_pool.empty()) {
       hipEvent_t a, b;
@@ -196,7 +209,7 @@ void prof_collect(bls_ctx* c) {
 int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
   int* d_r;
   SCR(S_INT, 4, d_r);
-  PROF(7, launch_final_check_wave(ctx->stream, f, n, d_r));
+  PROF(7, launch_final_check_wave(ctx->j->stream, f, n, d_r));
   int r = 0;
   CK(d2h(ctx, &r, d_r, sizeof r));
   return r ? 1 : 0;
@@ -216,7 +229,45 @@ __global__ void k_set_neg_g1(G1A* p) {
   std::lock_guard<std::mutex> lock_(ctx->mu);  \
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, hipGetLastError(), "hipSetDevice")
 
+// Points the call at job k (after API_ENTER); job 0 again on return.
+struct JobScope {
+  bls_ctx* c;
+  JobScope(bls_ctx* c_, int k) : c(c_) { c->j = &c->jobs[k]; }
+  ~JobScope() { c->j = &c->jobs[0]; }
+};
+#define JOB_ENTER(ctx, job)                                  \
+  API_ENTER(ctx);                                            \
+  if ((job) < 0 || (job) >= BLS_FAV_JOBS) return BLS_E_ARG;  \
+  JobScope job_scope_(ctx, job)
+
 extern "C" {
+
+static bool job_init(Job& J, int prio_hi) {
+  return hipStreamCreateWithFlags(&J.stream, hipStreamNonBlocking) == hipSuccess &&
+         hipStreamCreateWithFlags(&J.stream2, hipStreamNonBlocking) == hipSuccess &&
+         hipStreamCreateWithPriority(&J.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_join, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_sig, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_msm, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_gather, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_partial, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc((void**)&J.h_partial, 576, hipHostMallocDefault) == hipSuccess;
+}
+
+static void job_destroy(Job& J) {
+  hipStream_t ss[3] = {J.stream, J.stream2, J.stream3};
+  for (hipStream_t s : ss)
+    if (s) (void)hipStreamSynchronize(s);
+  for (auto& b : J.buf)
+    if (b.p) (void)hipFree(b.p);
+  hipEvent_t es[6] = {J.ev_fork, J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial};
+  for (hipEvent_t e : es)
+    if (e) (void)hipEventDestroy(e);
+  if (J.h_partial) (void)hipHostFree(J.h_partial);
+  for (hipStream_t s : ss)
+    if (s) (void)hipStreamDestroy(s);
+}
 
 int bls_ctx_create(int device, bls_ctx** out) {
   if (!out) return BLS_E_ARG;
@@ -229,16 +280,11 @@ int bls_ctx_create(int device, bls_ctx** out) {
   c->device = device;
   int prio_lo = 0, prio_hi = 0;  // the MSM branch is latency-bound: schedule it first
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_sig, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_msm, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gather, hipEventDisableTiming) != hipSuccess) {
-    delete c;
-    return BLS_E_DEVICE;
+  for (Job& J : c->jobs) {
+    if (!job_init(J, prio_hi)) {
+      bls_ctx_destroy(c);
+      return BLS_E_DEVICE;
+    }
   }
   *out = c;
   return 0;
@@ -247,9 +293,7 @@ int bls_ctx_create(int device, bls_ctx** out) {
 void bls_ctx_destroy(bls_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  for (auto& b : ctx->buf)
-    if (b.p) (void)hipFree(b.p);
+  for (Job& J : ctx->jobs) job_destroy(J);
   for (auto& p : ctx->prof_pending) ctx->prof_pool.push_back(p.second);
   for (auto& p : ctx->prof_pool) {
     (void)hipEventDestroy(p.first);
@@ -257,16 +301,6 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   }
   if (ctx->reg) (void)hipFree(ctx->reg);
   if (ctx->reg_ok) (void)hipFree(ctx->reg_ok);
-  (void)hipStreamSynchronize(ctx->stream2);
-  (void)hipStreamSynchronize(ctx->stream3);
-  (void)hipEventDestroy(ctx->ev_fork);
-  (void)hipEventDestroy(ctx->ev_join);
-  (void)hipEventDestroy(ctx->ev_sig);
-  (void)hipEventDestroy(ctx->ev_msm);
-  (void)hipEventDestroy(ctx->ev_gather);
-  (void)hipStreamDestroy(ctx->stream2);
-  (void)hipStreamDestroy(ctx->stream3);
-  (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
@@ -293,7 +327,7 @@ int bls_verify(bls_ctx* ctx, const uint8_t* pk48, const uint8_t* msg, size_t msg
   CK(h2d(ctx, d, pk48, 48));
   CK(h2d(ctx, d + 48, sig96, 96));
   CK(h2d(ctx, d + 144, msg, msg_len));
-  LK(launch_verify_single(ctx->stream, d, d + 144, (uint32_t)msg_len, d + 48, d_r));
+  LK(launch_verify_single(ctx->j->stream, d, d + 144, (uint32_t)msg_len, d + 48, d_r));
   int r = 0;
   CK(d2h(ctx, &r, d_r, sizeof r));
   return r ? 1 : 0;
@@ -315,10 +349,10 @@ int bls_fast_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, cons
   SCR(S_G1J, 1, apk);
   SCR(S_IN1, 96 + msg_len, d);
   SCR(S_INT, 4, d_r);
-  LK(launch_g1_sum_aff(ctx->stream, a, nullptr, n, tmp, apk));
+  LK(launch_g1_sum_aff(ctx->j->stream, a, nullptr, n, tmp, apk));
   CK(h2d(ctx, d, sig96, 96));
   CK(h2d(ctx, d + 96, msg, msg_len));
-  LK(launch_verify_apk(ctx->stream, apk, d + 96, (uint32_t)msg_len, d, d_r));
+  LK(launch_verify_apk(ctx->j->stream, apk, d + 96, (uint32_t)msg_len, d, d_r));
   int r = 0;
   CK(d2h(ctx, &r, d_r, sizeof r));
   return r ? 1 : 0;
@@ -354,17 +388,17 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   SCR(S_F_T, (n + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   CK(h2d(ctx, d_sig, sig96, 96));
-  LK(launch_sig_validate(ctx->stream, d_sig, 1, Q + n, d_sok));
+  LK(launch_sig_validate(ctx->j->stream, d_sig, 1, Q + n, d_sok));
   int sok = 0;
   CK(d2h(ctx, &sok, d_sok, sizeof sok));
   if (!sok) return 0;
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
-  LK(launch_hash_many(ctx->stream, d_msgs, d_offs, n, nullptr, 0, Q));
-  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->stream, P + n);
+  LK(launch_hash_many(ctx->j->stream, d_msgs, d_offs, n, nullptr, 0, Q));
+  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->j->stream, P + n);
   LK(hipGetLastError());
-  LK(launch_miller_wave(ctx->stream, P, Q, nullptr, n + 1, f));
-  LK(launch_fp12_prod_vm(ctx->stream, f, n + 1, ft, fo));
+  LK(launch_miller_wave(ctx->j->stream, P, Q, nullptr, n + 1, f));
+  LK(launch_fp12_prod_vm(ctx->j->stream, f, n + 1, ft, fo));
   return run_final_check(ctx, fo);
 }
 
@@ -383,13 +417,13 @@ int bls_aggregate(bls_ctx* ctx, const uint8_t* sigs96, size_t n, uint8_t* out96)
   SCR(S_G2J, 1, s);
   SCR(S_IN1, 96, d_out);
   CK(h2d(ctx, d_in, sigs96, 96 * n));
-  LK(launch_sig_validate(ctx->stream, d_in, n, a, d_ok));
+  LK(launch_sig_validate(ctx->j->stream, d_in, n, a, d_ok));
   std::vector<int> ok(n);
   CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
   for (size_t i = 0; i < n; i++)
     if (!ok[i]) return 0;
-  LK(launch_g2_sum_aff(ctx->stream, a, nullptr, n, tmp, s));
-  LK(launch_g2_compress(ctx->stream, s, d_out));
+  LK(launch_g2_sum_aff(ctx->j->stream, a, nullptr, n, tmp, s));
+  LK(launch_g2_compress(ctx->j->stream, s, d_out));
   CK(d2h(ctx, out96, d_out, 96));
   return 1;
 }
@@ -407,8 +441,8 @@ int bls_aggregate_pks(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, s);
   SCR(S_IN1, 48, d_out);
-  LK(launch_g1_sum_aff(ctx->stream, a, nullptr, n, tmp, s));
-  LK(launch_g1_compress(ctx->stream, s, d_out, nullptr));
+  LK(launch_g1_sum_aff(ctx->j->stream, a, nullptr, n, tmp, s));
+  LK(launch_g1_compress(ctx->j->stream, s, d_out, nullptr));
   CK(d2h(ctx, out48, d_out, 48));
   return 1;
 }
@@ -434,7 +468,7 @@ static int sign_impl(bls_ctx* ctx, const uint8_t* sks, const uint8_t* msgs, cons
   CK(h2d(ctx, d_sk, sks, 32 * n));
   CK(h2d(ctx, d_m, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs, (n + 1) * sizeof(uint64_t)));
-  LK(launch_sign_many(ctx->stream, d_sk, d_m, d_offs, n, d_out, d_ok));
+  LK(launch_sign_many(ctx->j->stream, d_sk, d_m, d_offs, n, d_out, d_ok));
   std::vector<int> ok(n);
   CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
   CK(d2h(ctx, out96, d_out, 96 * n));
@@ -471,7 +505,7 @@ static int sk_to_pk_impl(bls_ctx* ctx, const uint8_t* sks, size_t n, uint8_t* ou
   SCR(S_IN2, 48 * n, d_out);
   SCR(S_OK, n, d_ok);
   CK(h2d(ctx, d_sk, sks, 32 * n));
-  LK(launch_sk_to_pk_many(ctx->stream, d_sk, n, d_out, d_ok));
+  LK(launch_sk_to_pk_many(ctx->j->stream, d_sk, n, d_out, d_ok));
   std::vector<int> ok(n);
   CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
   CK(d2h(ctx, out48, d_out, 48 * n));
@@ -509,8 +543,8 @@ int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8
   CK(h2d(ctx, d_m, msg, msg_len));
   CK(h2d(ctx, d_dst, dst, dst_len));
   CK(h2d(ctx, d_offs, offs, sizeof offs));
-  LK(launch_hash_many(ctx->stream, d_m, d_offs, 1, d_dst, (uint32_t)dst_len, h));
-  LK(launch_g2_compress_aff(ctx->stream, h, d_out));
+  LK(launch_hash_many(ctx->j->stream, d_m, d_offs, 1, d_dst, (uint32_t)dst_len, h));
+  LK(launch_g2_compress_aff(ctx->j->stream, h, d_out));
   CK(d2h(ctx, out96, d_out, 96));
   return 1;
 }
@@ -520,7 +554,7 @@ int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out
   API_ENTER(ctx);
   if (!pks48 && n) return BLS_E_ARG;
   if (n > 0xffffffffu) return BLS_E_ARG;
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   if (ctx->reg) HIPCK(hipFree(ctx->reg));
   if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
   ctx->reg = nullptr;
@@ -533,10 +567,10 @@ int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out
   SCR(S_IN0, 48 * n, d_in);
   SCR(S_OK, n, d_ok);
   CK(h2d(ctx, d_in, pks48, 48 * n));
-  LK(launch_key_validate(ctx->stream, d_in, n, ctx->reg, d_ok));
-  LK(launch_status_to_u8(ctx->stream, d_ok, n, ctx->reg_ok));
+  LK(launch_key_validate(ctx->j->stream, d_in, n, ctx->reg, d_ok));
+  LK(launch_status_to_u8(ctx->j->stream, d_ok, n, ctx->reg_ok));
   if (out_valid) CK(d2h(ctx, out_valid, ctx->reg_ok, n));
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   ctx->reg_n = n;
   return 1;
 }
@@ -546,7 +580,7 @@ size_t bls_registry_size(bls_ctx* ctx) { return ctx ? ctx->reg_n : 0; }
 int bls_registry_generate(bls_ctx* ctx, uint64_t first_sk, size_t n, uint8_t* out_pks48) {
   API_ENTER(ctx);
   if (n > 0xffffffffu || first_sk == 0 || first_sk + n < first_sk || first_sk + n >= (1ull << 62)) return BLS_E_ARG;
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   if (ctx->reg) HIPCK(hipFree(ctx->reg));
   if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
   ctx->reg = nullptr;
@@ -558,16 +592,16 @@ int bls_registry_generate(bls_ctx* ctx, uint64_t first_sk, size_t n, uint8_t* ou
   uint8_t* d_out = nullptr;
   SCR(S_G1J_T, n, tmp);
   if (out_pks48) SCR(S_IN0, 48 * n, d_out);
-  LK(launch_registry_generate(ctx->stream, first_sk, n, tmp, ctx->reg, ctx->reg_ok, d_out));
+  LK(launch_registry_generate(ctx->j->stream, first_sk, n, tmp, ctx->reg, ctx->reg_ok, d_out));
   if (out_pks48) CK(d2h(ctx, out_pks48, d_out, 48 * n));
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   ctx->reg_n = n;
   return 1;
 }
 
 int bls_profile_enable(bls_ctx* ctx, int on) {
   API_ENTER(ctx);
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   prof_collect(ctx);
   ctx->prof_on = on != 0;
   for (int i = 0; i < 16; i++) {
@@ -579,7 +613,7 @@ int bls_profile_enable(bls_ctx* ctx, int on) {
 
 int bls_profile_read(bls_ctx* ctx, double* total_ms, uint64_t* counts, int max) {
   API_ENTER(ctx);
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   prof_collect(ctx);
   int n = max < PROF_N ? max : PROF_N;
   for (int i = 0; i < n; i++) {
@@ -625,7 +659,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_FPART, 1, fo);
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
-  hipStream_t st = ctx->stream, st2 = ctx->stream2, st3 = ctx->stream3;
+  hipStream_t st = ctx->j->stream, st2 = ctx->j->stream2, st3 = ctx->j->stream3;
   static const bool serial = getenv("BLS_SERIAL") != nullptr;  // profiling knob: one stream, no overlap
   if (serial) st2 = st3 = st;
   // Three branches:
@@ -633,19 +667,19 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   //   stream2: hash_to_G2 of every message
   //   stream3: signature decompression + RLC scalars -> MSM S = sum r_i sigma_i
   //            -> Miller loop of (-G1, S) -> f[B + 1]
-  HIPCK(hipEventRecord(ctx->ev_fork, st));
-  HIPCK(hipStreamWaitEvent(st2, ctx->ev_fork, 0));
-  HIPCK(hipStreamWaitEvent(st3, ctx->ev_fork, 0));
+  HIPCK(hipEventRecord(ctx->j->ev_fork, st));
+  HIPCK(hipStreamWaitEvent(st2, ctx->j->ev_fork, 0));
+  HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, H, flag));
-  HIPCK(hipEventRecord(ctx->ev_join, st2));
+  HIPCK(hipEventRecord(ctx->j->ev_join, st2));
   PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
-  HIPCK(hipEventRecord(ctx->ev_sig, st3));
+  HIPCK(hipEventRecord(ctx->j->ev_sig, st3));
   PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apka, status));
-  HIPCK(hipEventRecord(ctx->ev_gather, st));
+  HIPCK(hipEventRecord(ctx->j->ev_gather, st));
   // The MSM covers every decoded signature of a valid aggregate key, before
   // the subgroup checks: a decodable signature outside G2 stays in S, so the
   // batch check fails and fav_finish re-checks every item individually.
-  HIPCK(hipStreamWaitEvent(st3, ctx->ev_gather, 0));
+  HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_gather, 0));
   {
     ProfScope ps_(ctx, 11, st3);
     LK(launch_msm(st3, B, status, dstat, rsc, sig, msmu, msmf, saff));
@@ -653,17 +687,17 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     LK(hipGetLastError());
     LK(launch_miller_wave(st3, rP + B, saff, nullptr, 1, f + B + 1));
   }
-  HIPCK(hipEventRecord(ctx->ev_msm, st3));
-  HIPCK(hipStreamWaitEvent(st, ctx->ev_sig, 0));
+  HIPCK(hipEventRecord(ctx->j->ev_msm, st3));
+  HIPCK(hipStreamWaitEvent(st, ctx->j->ev_sig, 0));
   PROF(10, launch_sig_vm(st, B, status, dstat, apka, sig, rsc, rP));
   // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
-  HIPCK(hipStreamWaitEvent(st, ctx->ev_join, 0));
+  HIPCK(hipStreamWaitEvent(st, ctx->j->ev_join, 0));
   PROF(5, launch_miller2(st, rP, H, status, B, f));
   PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
-  HIPCK(hipStreamWaitEvent(st, ctx->ev_msm, 0));
+  HIPCK(hipStreamWaitEvent(st, ctx->j->ev_msm, 0));
   LK(launch_fp12_prod_vm(st, f + B, 2, ft, fo));
-  ctx->fav_B = B;
-  ctx->fav_ready = true;
+  ctx->j->fav_B = B;
+  ctx->j->fav_ready = true;
   *out_f = fo;
   return 0;
 }
@@ -677,12 +711,12 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
 // items among B this costs about 16 k log16(B / k) checks in log16(B) rounds
 // instead of B checks.  root_bad: the caller already knows the product fails.
 static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
-  const size_t B = ctx->fav_B;
-  const int* status = (const int*)ctx->buf[S_STATUS].p;
-  const uint64_t* rsc = (const uint64_t*)ctx->buf[S_RSC].p;
-  const G1A* rP = (const G1A*)ctx->buf[S_RP].p;
-  const G2A* H = (const G2A*)ctx->buf[S_H].p;
-  const G2A* sig = (const G2A*)ctx->buf[S_SIG].p;
+  const size_t B = ctx->j->fav_B;
+  const int* status = (const int*)ctx->j->buf[S_STATUS].p;
+  const uint64_t* rsc = (const uint64_t*)ctx->j->buf[S_RSC].p;
+  const G1A* rP = (const G1A*)ctx->j->buf[S_RP].p;
+  const G2A* H = (const G2A*)ctx->j->buf[S_H].p;
+  const G2A* sig = (const G2A*)ctx->j->buf[S_SIG].p;
   std::vector<size_t> off{0}, cnt{B};
   while (cnt.back() > 1) {
     off.push_back(off.back() + cnt.back());
@@ -702,7 +736,7 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   SCR(S_BSEL, B + 16, d_sel);
   SCR(S_BRES, B + 16, d_res);
   SCR(S_BBAD, B, d_bad);
-  hipStream_t st = ctx->stream;
+  hipStream_t st = ctx->j->stream;
   LK(launch_bisect_pairs(st, B, rsc, status, rP, H, sig, P2, Q2, st2));
   LK(launch_miller2(st, P2, Q2, st2, 2 * B, tree));
   for (size_t L = 0; L + 1 < cnt.size(); L++)
@@ -712,7 +746,7 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   std::vector<int> res;
   int L = (int)cnt.size() - 1;
   cand.push_back(0);
-  ctx->bis_checks = ctx->bis_rounds = 0;
+  ctx->j->bis_checks = ctx->j->bis_rounds = 0;
   auto children = [&](int lvl, uint32_t node, std::vector<uint32_t>& next) {
     for (size_t c = (size_t)node * 16; c < (size_t)node * 16 + 16 && c < cnt[lvl - 1]; c++) next.push_back((uint32_t)c);
   };
@@ -730,8 +764,8 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
     PROF(8, launch_final_check_sel(st, tree, d_sel, n, d_res));
     res.resize(n);
     CK(d2h(ctx, res.data(), d_res, 4 * n));
-    ctx->bis_checks += n;
-    ctx->bis_rounds += 1;
+    ctx->j->bis_checks += n;
+    ctx->j->bis_rounds += 1;
     std::vector<uint32_t> next;
     for (size_t k = 0; k < n; k++) {
       if (res[k]) continue;
@@ -747,15 +781,15 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
 }
 
 static int fav_finish(bls_ctx* ctx, int batch_ok, bool root_bad, uint8_t* d_out) {
-  if (!ctx->fav_ready) {
+  if (!ctx->j->fav_ready) {
     ctx->err = "no prepared FAV batch";
     return BLS_E_ARG;
   }
-  size_t B = ctx->fav_B;
-  int* status = (int*)ctx->buf[S_STATUS].p;
+  size_t B = ctx->j->fav_B;
+  int* status = (int*)ctx->j->buf[S_STATUS].p;
   if (batch_ok) {
-    ctx->bis_checks = ctx->bis_rounds = 0;
-    PROF(8, launch_status_to_u8(ctx->stream, status, B, d_out));
+    ctx->j->bis_checks = ctx->j->bis_rounds = 0;
+    PROF(8, launch_status_to_u8(ctx->j->stream, status, B, d_out));
     return 0;
   }
   return fav_bisect(ctx, root_bad, d_out);
@@ -823,8 +857,8 @@ int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const 
 
 int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds) {
   API_ENTER(ctx);
-  if (fe_checks) *fe_checks = ctx->bis_checks;
-  if (rounds) *rounds = ctx->bis_rounds;
+  if (fe_checks) *fe_checks = ctx->j->bis_checks;
+  if (rounds) *rounds = ctx->j->bis_rounds;
   return 0;
 }
 
@@ -840,7 +874,7 @@ void* bls_dev_alloc(bls_ctx* ctx, size_t bytes) {
 
 int bls_dev_free(bls_ctx* ctx, void* p) {
   API_ENTER(ctx);
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   HIPCK(hipFree(p));
   return 0;
 }
@@ -848,7 +882,7 @@ int bls_dev_free(bls_ctx* ctx, void* p) {
 int bls_h2d(bls_ctx* ctx, void* dst, const void* src, size_t bytes) {
   API_ENTER(ctx);
   CK(h2d(ctx, dst, src, bytes));
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   return 0;
 }
 
@@ -860,42 +894,96 @@ int bls_d2h(bls_ctx* ctx, void* dst, const void* src, size_t bytes) {
 
 int bls_sync(bls_ctx* ctx) {
   API_ENTER(ctx);
-  HIPCK(hipStreamSynchronize(ctx->stream));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
   return 0;
 }
 
-int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
-                              const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32,
-                              uint8_t* partial576) {
-  API_ENTER(ctx);
-  if (!d_offsets || !d_msgs32 || !d_sigs96 || !seed32 || !partial576 || !B) return BLS_E_ARG;
+// ---------------------------------------------- pipelined FAV batches --
+static int job_submit(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B, const uint8_t* d_msgs32,
+                      const uint8_t* d_sigs96, const uint8_t* seed32) {
+  if (!d_offsets || !d_msgs32 || !d_sigs96 || !seed32 || !B) return BLS_E_ARG;
   Fp12* f;
   CK(fav_prepare(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32, &f));
   uint8_t* d_b;
   SCR(S_BYTES, 576, d_b);
-  LK(launch_fp12_to_bytes(ctx->stream, f, d_b));
-  CK(d2h(ctx, partial576, d_b, 576));
+  Job& J = *ctx->j;
+  LK(launch_fp12_to_bytes(J.stream, f, d_b));
+  HIPCK(hipMemcpyAsync(J.h_partial, d_b, 576, hipMemcpyDeviceToHost, J.stream));
+  HIPCK(hipEventRecord(J.ev_partial, J.stream));
+  J.partial_pending = true;
   return 1;
 }
 
-int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
-  API_ENTER(ctx);
+static int job_partial(bls_ctx* ctx, uint8_t* partial576) {
+  Job& J = *ctx->j;
+  if (!partial576) return BLS_E_ARG;
+  if (!J.partial_pending) {
+    ctx->err = "no submitted FAV batch on this job";
+    return BLS_E_ARG;
+  }
+  HIPCK(hipEventSynchronize(J.ev_partial));
+  memcpy(partial576, J.h_partial, 576);
+  J.partial_pending = false;
+  return 1;
+}
+
+static int job_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
   if (!partials576 || !n) return BLS_E_ARG;
   uint8_t* d_b;
   Fp12* f;
   SCR(S_IN0, 576 * n, d_b);
   SCR(S_FCHK, n, f);
   CK(h2d(ctx, d_b, partials576, 576 * n));
-  PROF(9, launch_fp12_from_bytes(ctx->stream, d_b, n, f));
+  PROF(9, launch_fp12_from_bytes(ctx->j->stream, d_b, n, f));
   return run_final_check(ctx, f, (int)n);  // the n partials are multiplied inside the FE kernel
+}
+
+static int job_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
+  if (!d_out) return BLS_E_ARG;
+  CK(fav_finish(ctx, batch_ok, false, d_out));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  return 1;
+}
+
+int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
+                              const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32,
+                              uint8_t* partial576) {
+  API_ENTER(ctx);
+  if (!partial576) return BLS_E_ARG;
+  const int r = job_submit(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32);
+  if (r < 0) return r;
+  return job_partial(ctx, partial576);
+}
+
+int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
+  API_ENTER(ctx);
+  return job_check(ctx, partials576, n);
 }
 
 int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   API_ENTER(ctx);
-  if (!d_out) return BLS_E_ARG;
-  CK(fav_finish(ctx, batch_ok, false, d_out));
-  HIPCK(hipStreamSynchronize(ctx->stream));
-  return 1;
+  return job_finish(ctx, batch_ok, d_out);
+}
+
+int bls_fav_job_submit_dev(bls_ctx* ctx, int job, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
+                           const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32) {
+  JOB_ENTER(ctx, job);
+  return job_submit(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32);
+}
+
+int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576) {
+  JOB_ENTER(ctx, job);
+  return job_partial(ctx, partial576);
+}
+
+int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t n) {
+  JOB_ENTER(ctx, job);
+  return job_check(ctx, partials576, n);
+}
+
+int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out) {
+  JOB_ENTER(ctx, job);
+  return job_finish(ctx, batch_ok, d_out);
 }
 
 }  // extern "C"

@@ -37,6 +37,9 @@ extern "C" {
 
 typedef struct bls_ctx bls_ctx;
 
+/* FAV batches that may be in flight together on one context (bls_fav_job_*). */
+#define BLS_FAV_JOBS 2
+
 /* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
 int bls_ctx_create(int device, bls_ctx** out);
 void bls_ctx_destroy(bls_ctx* ctx);
@@ -138,6 +141,25 @@ int bls_partials_check(bls_ctx* ctx, const uint8_t* partials576, size_t n);
  * bls_partials_check; when 0 this shard is bisected (its own product is
  * re-checked first, so a bad shard elsewhere leaves these verdicts intact). */
 int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out);
+
+/* ---- pipelined FAV batches (device-resident inputs) --------------------
+ * The three phases above, split per job so that up to BLS_FAV_JOBS batches
+ * are in flight on one context: while job k's Miller product is gathered
+ * (RCCL) and final-exponentiated, job k+1's kernels already run on the job's
+ * own streams.  A job must be finished before it is submitted again; each
+ * job keeps its own per-item state for its finish/bisection.  Same meaning,
+ * return codes and verdicts as bls_fav_batch_partial_dev / bls_partials_check
+ * / bls_fav_batch_finish_dev (those are job 0, submitted and waited at once).
+ *   submit:  enqueue the batch, return at once (1 or BLS_E_*)
+ *   partial: wait for the job's 576-byte Miller product
+ *   check:   final exponentiation of the product of n partials on the job's
+ *            stream: 1 / 0
+ *   finish:  verdicts into d_out (bisection when batch_ok == 0); waits */
+int bls_fav_job_submit_dev(bls_ctx* ctx, int job, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
+                           const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32);
+int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576);
+int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t n);
+int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out);
 
 /* ---- tracing: hipEvent time per kernel of the FAV path ------------------ */
 int bls_profile_enable(bls_ctx* ctx, int on);  /* also resets the totals */
