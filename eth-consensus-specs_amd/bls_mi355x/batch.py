@@ -17,7 +17,7 @@ import numpy as np
 
 from . import _native
 
-FAV_JOBS = 2  # BLS_FAV_JOBS in include/blsmi355x.h: batches in flight on one context
+FAV_JOBS = 4  # BLS_FAV_JOBS in include/blsmi355x.h: batches in flight on one context
 
 
 def _ptr(a: np.ndarray):
@@ -199,24 +199,25 @@ class ResidentFavBatch:
         c.check(c.lib.bls_fav_job_finish_dev(c.h, job, 1 if batch_ok else 0, self.outs[job].ptr))
         self.last_job = job
 
-    def run_pipelined(self, seeds, exchange=None) -> list:
-        """One pass over the batch per seed, pass k+1 submitted before pass k is
-        final-exponentiated (its front kernels overlap pass k's tail).
-        exchange(partial) -> concatenated partials of all ranks (multi-GPU
-        all-gather); every pass is complete (verdicts written) on return."""
+    def run_pipelined(self, seeds, exchange=None, depth: int = FAV_JOBS) -> list:
+        """One pass over the batch per seed with up to `depth` passes in flight:
+        pass k+1.. are submitted before pass k is final-exponentiated (their
+        front kernels overlap pass k's tail).  exchange(partial) -> concatenated
+        partials of all ranks (multi-GPU all-gather); every pass is complete
+        (verdicts written) on return."""
         seeds = list(seeds)
+        depth = max(1, min(depth, FAV_JOBS))
         oks = []
-        if not seeds:
-            return oks
-        self.submit(0, seeds[0])
+        for k in range(min(depth, len(seeds))):
+            self.submit(k % FAV_JOBS, seeds[k])
         for k in range(len(seeds)):
             job = k % FAV_JOBS
-            if k + 1 < len(seeds):
-                self.submit((k + 1) % FAV_JOBS, seeds[k + 1])
             part = self.job_partial(job)
             ok = self.job_check(job, exchange(part) if exchange else part)
             self.job_finish(job, ok)
             oks.append(ok)
+            if k + depth < len(seeds):
+                self.submit((k + depth) % FAV_JOBS, seeds[k + depth])
         return oks
 
     def verdicts(self) -> np.ndarray:

@@ -38,7 +38,7 @@ extern "C" {
 typedef struct bls_ctx bls_ctx;
 
 /* FAV batches that may be in flight together on one context (bls_fav_job_*). */
-#define BLS_FAV_JOBS 2
+#define BLS_FAV_JOBS 4
 
 /* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
 int bls_ctx_create(int device, bls_ctx** out);
