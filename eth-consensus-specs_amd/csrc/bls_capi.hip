@@ -19,7 +19,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT,
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
   NSLOT
@@ -638,7 +638,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   G2A *sig, *H, *saff;
   Fp12 *f, *ft, *fo;
   Fp* U;
-  Fd* msmf;
+  Fd *msmf, *hcf;
   uint64_t* rsc;
   uint32_t* msmu;
   uint8_t* d_seed;
@@ -652,6 +652,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_RSC, B, rsc);
   SCR(S_MSMU, msm_scratch_u32(B), msmu);
   SCR(S_MSMF, msm_scratch_fd(), msmf);
+  SCR(S_HCF, h2c_scratch_fd(B), hcf);
   SCR(S_SAFF, 1, saff);
   SCR(S_MSTAT, B, dstat);
   SCR(S_F, B + 2, f);
@@ -670,7 +671,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   HIPCK(hipEventRecord(ctx->j->ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, ctx->j->ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_fork, 0));
-  PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, H, flag));
+  PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, hcf, H, flag));
   HIPCK(hipEventRecord(ctx->j->ev_join, st2));
   PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
   HIPCK(hipEventRecord(ctx->j->ev_sig, st3));

@@ -41,21 +41,51 @@ __global__ void __launch_bounds__(64) k_h2c_sswu(size_t B, const uint8_t* msgs32
   o[3] = y.c1;
 }
 
-// (2) isogeny, sum, cofactor clearing and affine conversion on the VM.
+// (2) isogeny, sum, cofactor clearing and affine conversion on the VM, in
+// phases (HBM staging in Fd form, 24 slots per item: Q | M | A | C):
+//   k_h2c_iso    U -> Q = iso(U0) + iso(U1), flag
+//   k_g2x_chain  M = [|x|] Q
+//   k_h2c_pre    Q, M -> A, C  (h_eff Q = C - [|x|] A)
+//   k_g2x_chain  M = [|x|] A
+//   k_h2c_post   C, M -> H affine
+// The [|x|] chains are 63 dependent doubling levels of 10-12 products per
+// item; their own kernel has a compact layout (WL_XC: base | M | scratch) so
+// 5 items share a workgroup instead of 2.
 // flag[i] = 1 when an isogeny denominator vanished (the item is recomputed
 // by k_h2c_fallback; unreachable for SHA-256 outputs in practice).
+constexpr int HCF = 24;  // staged Fd slots per item
+constexpr int HCF_Q = 0, HCF_M = 6, HCF_A = 12, HCF_C = 18;
+
 template <int G>
-__global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, const Fp* U, G2A* H, int* flag) {
+__device__ __forceinline__ void hc_stage_in(Fd* s, const int* live, size_t i0, const Fd* hf, int src, int dst, int n) {
+  for (int k = threadIdx.x; k < n * G; k += 64) {
+    const int g = k / n, j = k % n;
+    s[WP_NCONST + g * WL_HC_STRIDE + dst + j] = live[g] ? hf[HCF * (i0 + g) + src + j] : fd_zero();
+  }
+}
+template <int G>
+__device__ __forceinline__ void hc_stage_out(const Fd* s, size_t B, size_t i0, Fd* hf, int src, int dst, int n) {
+  for (int k = threadIdx.x; k < n * G; k += 64) {
+    const int g = k / n, j = k % n;
+    if (i0 + g < B) hf[HCF * (i0 + g) + dst + j] = s[WP_NCONST + g * WL_HC_STRIDE + src + j];
+  }
+}
+template <int G>
+__device__ __forceinline__ void hc_live(int* live, size_t i0, size_t B, const int* status) {
+  if (threadIdx.x < G) {
+    const size_t i = i0 + threadIdx.x;
+    live[threadIdx.x] = i < B && (!status || status[i]);
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(64, 3) k_h2c_iso(size_t B, const int* status, const Fp* U, Fd* hf, int* flag) {
   __shared__ Fd s[WP_NCONST + G * WL_HC_STRIDE];
   __shared__ int live[G];
   const int lane = threadIdx.x;
   const size_t i0 = (size_t)blockIdx.x * G;
+  hc_live<G>(live, i0, B, status);
   vm_load_consts(s);
-  if (lane < G) {
-    const size_t i = i0 + lane;
-    live[lane] = i < B && (!status || status[i]);
-  }
-  __syncthreads();
   const int item0 = WP_NCONST;
   for (int k = lane; k < 8 * G; k += 64) {
     const int g = k >> 3, j = k & 7;
@@ -63,19 +93,66 @@ __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, c
   }
   __syncthreads();
   vm_run<G>(VM_PROG(HC_ISO), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XQ_0), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XQ_1), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XQ_2), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XQ_3), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XQ_4), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XQ_5), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_PRE), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XA_0), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XA_1), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XA_2), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XA_3), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XA_4), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_XA_5), s, item0, WL_HC_STRIDE, nullptr);
+  hc_stage_out<G>(s, B, i0, hf, WL_HC_Q, HCF_Q, 6);
+  if (lane < G && i0 + lane < B) {
+    const Fd* r = s + item0 + lane * WL_HC_STRIDE;
+    const bool bad = fd_is_zero(r[WL_HC_IZ]) && fd_is_zero(r[WL_HC_IZ + 1]);
+    const bool bad2 = fd_is_zero(r[WL_HC_IZ + 2]) && fd_is_zero(r[WL_HC_IZ + 3]);
+    flag[i0 + lane] = live[lane] && (bad || bad2);
+  }
+}
+
+// M = [|x|] B for projective E2 points staged as Fd slots (item stride HCF).
+template <int G>
+__global__ void __launch_bounds__(64) k_g2x_chain(size_t B, Fd* hf, int src, int dst) {
+  __shared__ Fd s[WP_NCONST + G * WL_XC_STRIDE];
+  const int lane = threadIdx.x;
+  const size_t i0 = (size_t)blockIdx.x * G;
+  const int item0 = WP_NCONST;
+  for (int k = lane; k < 6 * G; k += 64) {
+    const int g = k / 6, j = k % 6;
+    s[item0 + g * WL_XC_STRIDE + WL_XC_B + j] = i0 + g < B ? hf[HCF * (i0 + g) + src + j] : fd_zero();
+  }
+  vm_load_consts(s);  // ends with a barrier
+  vm_run<G>(VM_PROG(XC_0), s, item0, WL_XC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(XC_1), s, item0, WL_XC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(XC_2), s, item0, WL_XC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(XC_3), s, item0, WL_XC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(XC_4), s, item0, WL_XC_STRIDE, nullptr);
+  vm_run<G>(VM_PROG(XC_5), s, item0, WL_XC_STRIDE, nullptr);
+  for (int k = lane; k < 6 * G; k += 64) {
+    const int g = k / 6, j = k % 6;
+    if (i0 + g < B) hf[HCF * (i0 + g) + dst + j] = s[item0 + g * WL_XC_STRIDE + WL_XC_M + j];
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(64, 3) k_h2c_pre(size_t B, const int* status, Fd* hf) {
+  __shared__ Fd s[WP_NCONST + G * WL_HC_STRIDE];
+  __shared__ int live[G];
+  const size_t i0 = (size_t)blockIdx.x * G;
+  hc_live<G>(live, i0, B, status);
+  vm_load_consts(s);
+  hc_stage_in<G>(s, live, i0, hf, HCF_Q, WL_HC_Q, 6);
+  hc_stage_in<G>(s, live, i0, hf, HCF_M, WL_HC_M, 6);
+  __syncthreads();
+  vm_run<G>(VM_PROG(HC_PRE), s, WP_NCONST, WL_HC_STRIDE, nullptr);
+  hc_stage_out<G>(s, B, i0, hf, WL_HC_A, HCF_A, 6);
+  hc_stage_out<G>(s, B, i0, hf, WL_HC_C, HCF_C, 6);
+}
+
+template <int G>
+__global__ void __launch_bounds__(64, 3) k_h2c_post(size_t B, const int* status, const Fd* hf, G2A* H) {
+  __shared__ Fd s[WP_NCONST + G * WL_HC_STRIDE];
+  __shared__ int live[G];
+  const int lane = threadIdx.x;
+  const size_t i0 = (size_t)blockIdx.x * G;
+  hc_live<G>(live, i0, B, status);
+  vm_load_consts(s);
+  hc_stage_in<G>(s, live, i0, hf, HCF_C, WL_HC_C, 6);
+  hc_stage_in<G>(s, live, i0, hf, HCF_M, WL_HC_M, 6);
+  __syncthreads();
+  const int item0 = WP_NCONST;
   vm_run<G>(VM_PROG(HC_POST), s, item0, WL_HC_STRIDE, nullptr);
   vm_run<G>(VM_PROG(HC_NORM), s, item0, WL_HC_STRIDE, nullptr);
   if (lane < G) {  // 1 / norm(Z): one inversion per item
@@ -89,8 +166,6 @@ __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, c
     const size_t i = i0 + lane;
     if (i < B) {
       const Fd* r = s + item0 + lane * WL_HC_STRIDE;
-      const bool bad = fd_is_zero(r[WL_HC_IZ]) && fd_is_zero(r[WL_HC_IZ + 1]);
-      const bool bad2 = fd_is_zero(r[WL_HC_IZ + 2]) && fd_is_zero(r[WL_HC_IZ + 3]);
       const bool inf = fd_is_zero(r[WL_HC_N]);
       G2A h;
       h.x = Fp2{fp_from_fd(r[WL_HC_XY]), fp_from_fd(r[WL_HC_XY + 1])};
@@ -101,7 +176,6 @@ __global__ void __launch_bounds__(64, 3) k_h2c_vm(size_t B, const int* status, c
         h.y = fp2_zero();
       }
       H[i] = h;
-      flag[i] = live[lane] && (bad || bad2);
     }
   }
 }
@@ -212,25 +286,46 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const i
 }
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+static int env_int_or(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
 static int env_g(const char* name, int dflt) {
   const char* v = getenv(name);
   const int g = v ? atoi(v) : dflt;
   return (g == 2 || g == 4 || g == 6) ? g : dflt;
 }
 
-hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, G2A* H, int* flag) {
+size_t h2c_scratch_fd(size_t B) { return (size_t)HCF * B; }
+
+template <int G>
+static hipError_t launch_h2c_phases(hipStream_t st, size_t B, const int* status, const Fp* U, Fd* hf, G2A* H,
+                                    int* flag, int xg) {
+  hipLaunchKernelGGL(k_h2c_iso<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, U, hf, flag);
+  for (int pass = 0; pass < 2; pass++) {  // M = [|x|] Q, then M = [|x|] A
+    const int src = pass ? HCF_A : HCF_Q;
+    if (xg == 4)
+      hipLaunchKernelGGL(k_g2x_chain<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, hf, src, HCF_M);
+    else if (xg == 6)
+      hipLaunchKernelGGL(k_g2x_chain<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, hf, src, HCF_M);
+    else
+      hipLaunchKernelGGL(k_g2x_chain<5>, dim3(nblk(B, 5)), dim3(64), 0, st, B, hf, src, HCF_M);
+    if (!pass) hipLaunchKernelGGL(k_h2c_pre<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf);
+  }
+  hipLaunchKernelGGL(k_h2c_post<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
+                      int* flag) {
   if (!B) return hipSuccess;
   hipLaunchKernelGGL(k_h2c_sswu, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs32, status, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  static const int hg = env_g("BLS_H2C_G", 2);  // tuning knob: items per workgroup
-  if (hg == 4)
-    hipLaunchKernelGGL(k_h2c_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, U, H, flag);
-  else if (hg == 6)
-    hipLaunchKernelGGL(k_h2c_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, U, H, flag);
-  else
-    hipLaunchKernelGGL(k_h2c_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, U, H, flag);
-  e = hipGetLastError();
+  static const int hg = env_g("BLS_H2C_G", 2);  // tuning knobs: items per workgroup
+  static const int xg = env_int_or("BLS_XC_G", 5);
+  e = hg == 4 ? launch_h2c_phases<4>(st, B, status, U, hf, H, flag, xg)
+              : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_h2c_fallback, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, flag, H);
   return hipGetLastError();

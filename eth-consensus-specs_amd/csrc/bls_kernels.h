@@ -24,7 +24,10 @@ hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, F
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96);
 hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok, uint8_t* out48);
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
-hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, G2A* H, int* flag);
+// hf: h2c_scratch_fd(B) Fd slots of staging between the hash_to_G2 phases
+size_t h2c_scratch_fd(size_t B);
+hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
+                      int* flag);
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat);
 hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff, const G2A* sig, const uint64_t* rsc, G1A* rP);
 size_t msm_scratch_u32(size_t B);

@@ -966,6 +966,31 @@ def compile_program(name, builder, frames, alias=None, schedule="asap"):
     work = [a for a in need if c.atoms[a][0] in ("prod", "lin", "sel", "lut")]
     for a in work:
         lvl(a)
+    if schedule.startswith("list:"):
+        # list scheduling with at most W ops per level (W = 64 / G fills one
+        # pass of a G-item workgroup): ready ops by decreasing height (longest
+        # path to the end of the program), so narrow dependency-bound levels
+        # are padded with work that the ASAP levelling put in wide levels
+        W = int(schedule.split(":")[1])
+        users = defaultdict(list)
+        for a in work:
+            for s_ in deps(a):
+                users[s_].append(a)
+        height = {}
+        for a in sorted(work, key=lambda a: -level[a]):
+            height[a] = 1 + max([height[u] for u in users.get(a, ())] or [0])
+        placed = {}
+        rem = set(work)
+        L = 0
+        while rem:
+            L += 1
+            ready = [a for a in rem
+                     if all(c.atoms[d][0] in ("in", "const") or placed.get(d, L) < L for d in deps(a))]
+            ready.sort(key=lambda a: (-height[a], a))
+            for a in ready[:W]:
+                placed[a] = L
+                rem.discard(a)
+        level.update(placed)
     if schedule == "alap":
         # as late as possible (within the ASAP depth): an op moves to one level
         # before its earliest consumer, so values live shorter (fewer LDS slots)
@@ -1233,6 +1258,12 @@ def define_instances(progs):
         nm = f"G2X_{k}{'A' if add else ''}"
         instance(f"HC_XQ_{i}", nm, [H["Q"] if i == 0 else H["M"], H["Q"], H["M"]], H["S"])
         instance(f"HC_XA_{i}", nm, [H["A"] if i == 0 else H["M"], H["A"], H["M"]], H["S"])
+    # [|x|] chains of cofactor clearing as their own kernel (k_g2x_chain):
+    # base | M | scratch only, so several more items share an LDS budget
+    xs = max(sc[n] for n in sc if n.startswith("G2X_"))
+    layout("XC", B=0, M=6, S=12, STRIDE=12 + xs)
+    for i, (k, add) in enumerate(X_RUNS):  # M = [|x|] B
+        instance(f"XC_{i}", f"G2X_{k}{'A' if add else ''}", [0 if i == 0 else 6, 0, 6], 12)
     instance("HC_PRE", "CLEAR_PRE", [H["Q"], H["M"], H["A"], H["C"]], H["S"])
     instance("HC_POST", "CLEAR_POST", [H["C"], H["M"], H["H"]], H["S"])
     instance("HC_NORM", "FP2_NORM", [H["H"] + 4, H["N"]], H["S"])
