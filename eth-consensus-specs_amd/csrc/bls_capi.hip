@@ -19,7 +19,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF,
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
   NSLOT
@@ -633,7 +633,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     return BLS_E_NOREG;
   }
   int *status, *flag, *dstat;
-  G1P* apka;
+  G1P *apka, *rpj;
   G1A* rP;
   G2A *sig, *H, *saff;
   Fp12 *f, *ft, *fo;
@@ -653,6 +653,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_MSMU, msm_scratch_u32(B), msmu);
   SCR(S_MSMF, msm_scratch_fd(), msmf);
   SCR(S_HCF, h2c_scratch_fd(B), hcf);
+  SCR(S_RPJ, B, rpj);
   SCR(S_SAFF, 1, saff);
   SCR(S_MSTAT, B, dstat);
   SCR(S_F, B + 2, f);
@@ -690,7 +691,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   }
   HIPCK(hipEventRecord(ctx->j->ev_msm, st3));
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_sig, 0));
-  PROF(10, launch_sig_vm(st, B, status, dstat, apka, sig, rsc, rP));
+  PROF(10, launch_sig_vm(st, B, status, dstat, apka, sig, rsc, rpj, rP));
   // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_join, 0));
   PROF(5, launch_miller2(st, rP, H, status, B, f));

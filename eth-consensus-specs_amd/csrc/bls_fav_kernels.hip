@@ -142,42 +142,39 @@ __global__ void __launch_bounds__(64, 3) k_h2c_pre(size_t B, const int* status, 
 }
 
 template <int G>
-__global__ void __launch_bounds__(64, 3) k_h2c_post(size_t B, const int* status, const Fd* hf, G2A* H) {
+__global__ void __launch_bounds__(64, 3) k_h2c_post(size_t B, const int* status, Fd* hf) {
   __shared__ Fd s[WP_NCONST + G * WL_HC_STRIDE];
   __shared__ int live[G];
-  const int lane = threadIdx.x;
   const size_t i0 = (size_t)blockIdx.x * G;
   hc_live<G>(live, i0, B, status);
   vm_load_consts(s);
   hc_stage_in<G>(s, live, i0, hf, HCF_C, WL_HC_C, 6);
   hc_stage_in<G>(s, live, i0, hf, HCF_M, WL_HC_M, 6);
   __syncthreads();
-  const int item0 = WP_NCONST;
-  vm_run<G>(VM_PROG(HC_POST), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_NORM), s, item0, WL_HC_STRIDE, nullptr);
-  if (lane < G) {  // 1 / norm(Z): one inversion per item
-    Fd* r = s + item0 + lane * WL_HC_STRIDE;
-    r[WL_HC_NI] = fd_from_fp(fp_inv(fp_from_fd(r[WL_HC_N])));
-  }
-  __syncthreads();
-  vm_run<G>(VM_PROG(HC_INVFIN), s, item0, WL_HC_STRIDE, nullptr);
-  vm_run<G>(VM_PROG(HC_TOAFF), s, item0, WL_HC_STRIDE, nullptr);
-  if (lane < G) {
-    const size_t i = i0 + lane;
-    if (i < B) {
-      const Fd* r = s + item0 + lane * WL_HC_STRIDE;
-      const bool inf = fd_is_zero(r[WL_HC_N]);
-      G2A h;
-      h.x = Fp2{fp_from_fd(r[WL_HC_XY]), fp_from_fd(r[WL_HC_XY + 1])};
-      h.y = Fp2{fp_from_fd(r[WL_HC_XY + 2]), fp_from_fd(r[WL_HC_XY + 3])};
-      h.inf = inf || !live[lane];
-      if (!live[lane]) {
-        h.x = fp2_zero();
-        h.y = fp2_zero();
-      }
-      H[i] = h;
+  vm_run<G>(VM_PROG(HC_POST), s, WP_NCONST, WL_HC_STRIDE, nullptr);
+  hc_stage_out<G>(s, B, i0, hf, WL_HC_H, HCF_A, 6);  // projective H over the dead A slots
+}
+
+// Affine conversion, one lane per item: 1/Z = conj(Z) / norm(Z) with one
+// binary-GCD inversion.  Inversions are long per-item chains: here the 64
+// lanes of a wave carry 64 items, where a VM workgroup would run them on
+// only G of its lanes.
+__global__ void __launch_bounds__(64) k_h2c_affine(size_t B, const int* status, const Fd* hf, G2A* H) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B) return;
+  G2A h{fp2_zero(), fp2_zero(), true};
+  if (!status || status[i]) {
+    const Fd* r = hf + HCF * i + HCF_A;
+    const Fp2 X{fp_from_fd(r[0]), fp_from_fd(r[1])}, Y{fp_from_fd(r[2]), fp_from_fd(r[3])};
+    const Fp2 Z{fp_from_fd(r[4]), fp_from_fd(r[5])};
+    const Fp n = fp2_norm(Z);
+    if (!fp_is_zero(n)) {
+      const Fp ni = fp_inv(n);
+      const Fp2 zi{fp_mul(Z.c0, ni), fp_neg(fp_mul(Z.c1, ni))};
+      h = G2A{fp2_mul(X, zi), fp2_mul(Y, zi), false};
     }
   }
+  H[i] = h;
 }
 
 __global__ void __launch_bounds__(64) k_h2c_fallback(size_t B, const uint8_t* msgs32, const int* flag, G2A* H) {
@@ -223,7 +220,7 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
 // affine.  sum r_i sigma_i is the batch MSM (bls_msm.hip).
 template <int G>
 __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const int* dstat, const G1P* apk,
-                                                 const G2A* sig, const uint64_t* rsc, G1A* rP) {
+                                                 const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   __shared__ Fd s[WP_NCONST + G * WL_SG_STRIDE];
   __shared__ int live[G];
   __shared__ uint32_t pred[G];
@@ -266,12 +263,6 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const i
   }
   vm_run<G>(VM_PROG(SG_SUBCHK), s, item0, WL_SG_STRIDE, nullptr);
   if (lane < G) {
-    Fd* e = s + item0 + lane * WL_SG_STRIDE;
-    e[WL_SG_NI] = fd_from_fp(fp_inv(fp_from_fd(e[WL_SG_R + 2])));
-  }
-  __syncthreads();
-  vm_run<G>(VM_PROG(SG_TOAFF), s, item0, WL_SG_STRIDE, nullptr);
-  if (lane < G) {
     const size_t i = i0 + lane;
     if (i < B) {
       const Fd* e = s + item0 + lane * WL_SG_STRIDE;
@@ -279,10 +270,23 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const i
       // sigma in G2  <=>  psi(sigma) == -[|x|] sigma  (differences zero, M not the identity)
       for (int j = 0; j < 4; j++) ok = ok && fd_is_zero(e[WL_SG_D + j]);
       ok = ok && !(fd_is_zero(e[WL_SG_D + 4]) && fd_is_zero(e[WL_SG_D + 5]));
-      rP[i] = ok ? G1A{fp_from_fd(e[WL_SG_XY1]), fp_from_fd(e[WL_SG_XY1 + 1]), false} : G1A{fp_zero(), fp_zero(), true};
+      rPj[i] = G1P{fp_from_fd(e[WL_SG_R]), fp_from_fd(e[WL_SG_R + 1]), fp_from_fd(e[WL_SG_R + 2])};
       status[i] = ok ? 1 : 0;
     }
   }
+}
+
+// r_i apk_i to affine, one lane per item (see k_h2c_affine).
+__global__ void __launch_bounds__(64) k_g1_affine(size_t B, const int* status, const G1P* rPj, G1A* rP) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B) return;
+  G1A o{fp_zero(), fp_zero(), true};
+  if (status[i]) {
+    const G1P q = rPj[i];
+    const Fp zi = fp_inv(q.z);
+    o = G1A{fp_mul(q.x, zi), fp_mul(q.y, zi), false};
+  }
+  rP[i] = o;
 }
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
@@ -312,7 +316,8 @@ static hipError_t launch_h2c_phases(hipStream_t st, size_t B, const int* status,
       hipLaunchKernelGGL(k_g2x_chain<5>, dim3(nblk(B, 5)), dim3(64), 0, st, B, hf, src, HCF_M);
     if (!pass) hipLaunchKernelGGL(k_h2c_pre<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf);
   }
-  hipLaunchKernelGGL(k_h2c_post<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf, H);
+  hipLaunchKernelGGL(k_h2c_post<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf);
+  hipLaunchKernelGGL(k_h2c_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, H);
   return hipGetLastError();
 }
 
@@ -339,15 +344,16 @@ hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, co
 }
 
 hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff,
-                         const G2A* sig, const uint64_t* rsc, G1A* rP) {
+                         const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP) {
   if (!B) return hipSuccess;
   static const int sg = env_g("BLS_SIG_G", 4);  // tuning knob: items per workgroup
   if (sg == 4)
-    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rP);
+    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
   else if (sg == 6)
-    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rP);
+    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
   else
-    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rP);
+    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
+  hipLaunchKernelGGL(k_g1_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, rPj, rP);
   return hipGetLastError();
 }
 

@@ -29,7 +29,9 @@ size_t h2c_scratch_fd(size_t B);
 hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
                       int* flag);
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat);
-hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff, const G2A* sig, const uint64_t* rsc, G1A* rP);
+// rPj: B projective scratch points (r_i apk_i before the affine conversion)
+hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff, const G2A* sig,
+                         const uint64_t* rsc, G1P* rPj, G1A* rP);
 size_t msm_scratch_u32(size_t B);
 size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);

@@ -7,7 +7,7 @@ run() {
   python -c "import json;d=json.load(open('gpurun_out/exp4/o.json'));print('$*',d['value'],d['ms_per_step'])"
 }
 run X=1
-run BLS_XC_G=4
+run BLS_H2C_G=4 BLS_XC_G=6
 run BLS_XC_G=6
 run BLS_H2C_G=4
-run BLS_SERIAL=1 X=2 
+run BLS_SIG_G=6

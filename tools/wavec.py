@@ -1248,16 +1248,11 @@ def define_instances(progs):
         cur = R(2) if i == 0 else R(1)
         instance(f"FE_POWX_{i}", nm, [cur, R(2), R(1)], 84)
     instance("FE_CUBE", "CYC_1M", [R(0), R(0), R(5)], 84)
-    # hash_to_G2 tail: SSWU points | Q | M | A | C | H | izs | Z (norm in) | N | NI | ZI | XY | scratch
-    H = dict(U=0, Q=8, M=14, A=20, C=26, H=32, IZ=38, N=42, NI=43, ZI=44, XY=46, S=50)
-    hs = max(sc["ISO_PAIR"], sc["CLEAR_PRE"], sc["CLEAR_POST"], sc["FP2_NORM"], sc["FP2_INVFIN"],
-             sc["G2_TOAFF"], *[sc[n] for n in sc if n.startswith("G2X_")])
+    # hash_to_G2 phases (k_h2c_iso / _pre / _post): SSWU points | Q | M | A | C | H | izs | scratch
+    H = dict(U=0, Q=8, M=14, A=20, C=26, H=32, IZ=38, S=42)
+    hs = max(sc["ISO_PAIR"], sc["CLEAR_PRE"], sc["CLEAR_POST"])
     layout("HC", STRIDE=H["S"] + hs, **H)
     instance("HC_ISO", "ISO_PAIR", [H["U"], H["Q"], H["IZ"]], H["S"])
-    for i, (k, add) in enumerate(X_RUNS):  # M = [|x|] Q  and later  M = [|x|] A
-        nm = f"G2X_{k}{'A' if add else ''}"
-        instance(f"HC_XQ_{i}", nm, [H["Q"] if i == 0 else H["M"], H["Q"], H["M"]], H["S"])
-        instance(f"HC_XA_{i}", nm, [H["A"] if i == 0 else H["M"], H["A"], H["M"]], H["S"])
     # [|x|] chains of cofactor clearing as their own kernel (k_g2x_chain):
     # base | M | scratch only, so several more items share an LDS budget
     xs = max(sc[n] for n in sc if n.startswith("G2X_"))
@@ -1266,17 +1261,13 @@ def define_instances(progs):
         instance(f"XC_{i}", f"G2X_{k}{'A' if add else ''}", [0 if i == 0 else 6, 0, 6], 12)
     instance("HC_PRE", "CLEAR_PRE", [H["Q"], H["M"], H["A"], H["C"]], H["S"])
     instance("HC_POST", "CLEAR_POST", [H["C"], H["M"], H["H"]], H["S"])
-    instance("HC_NORM", "FP2_NORM", [H["H"] + 4, H["N"]], H["S"])
-    instance("HC_INVFIN", "FP2_INVFIN", [H["H"] + 4, H["NI"], H["ZI"]], H["S"])
-    instance("HC_TOAFF", "G2_TOAFF", [H["H"], H["ZI"], H["XY"]], H["S"])
-    # signature side: sigma | apk | M | R | D (subgroup check) | NI | XY1 | scratch
-    G = dict(SIG=0, APK=4, M=7, R=13, D=16, NI=22, XY1=23, SC=25)
-    gs = max(sc["SIG_STEP0"], sc["SIG_STEP1"], sc["SIG_STEP2"], sc["G2_SUBCHK"], sc["G1_TOAFF"])
+    # signature side: sigma | apk | M | R | D (subgroup check) | scratch
+    G = dict(SIG=0, APK=4, M=7, R=13, D=16, SC=22)
+    gs = max(sc["SIG_STEP0"], sc["SIG_STEP1"], sc["SIG_STEP2"], sc["G2_SUBCHK"])
     layout("SG", STRIDE=G["SC"] + gs, **G)
     for m in range(3):
         instance(f"SG_STEP{m}", f"SIG_STEP{m}", [G["SIG"], G["APK"], G["M"], G["R"]], G["SC"])
     instance("SG_SUBCHK", "G2_SUBCHK", [G["SIG"], G["M"], G["D"]], G["SC"])
-    instance("SG_TOAFF", "G1_TOAFF", [G["R"], G["NI"], G["XY1"]], G["SC"])
     # MSM bucket accumulation: R | Q | scratch
     layout("MB", R=0, Q=6, S=10, STRIDE=10 + sc["G2_ADDAFF_SEL"])
     instance("MB_ADD", "G2_ADDAFF_SEL", [0, 6], 10)
