@@ -37,6 +37,8 @@ METRIC = "BLS sig verifications/sec (FastAggregateVerify, 1/8 GPU) + % int VALU 
 PEAK_INT_OPS = 256 * 4 * 32 / 2 * 2.4e9  # v_mad_u64_u32 is half rate on gfx950: 39.3e12 lane-ops/s
 FME_OPS = 288  # one 381-bit Montgomery multiplication = 288 v_mad_u64_u32
 SHA_OPS = 2400  # one SHA-256 compression
+MEASURED_MAD_OPS = 31.3e12  # sustained v_mad_u64_u32 lane-ops/s, profiles/r01_s2_madrate_microbench.txt
+GATHER_BYTES_PER_KEY = 4 + 96 + 1  # u32 index + affine (x, y) + validity byte
 
 
 def model_fme(n: int):
@@ -151,6 +153,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight (no overlap of passes)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel hipEvent timing")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batch call")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -248,6 +251,22 @@ def main():
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4), "peak": round(PEAK_INT_OPS / 1e12, 2),
                 "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5), "traffic": None,
                 "ops_per_launch": ops, "avg_launch_ms": round(avg_s * 1e3, 4)}
+    if roof is not None:
+        roof["frac_of_measured_mad_rate"] = round(roof["achieved"] * 1e12 / MEASURED_MAD_OPS, 5)
+    # secondary figure: algorithmic HBM bytes of the registry gather per launch / its duration
+    gather_gbs = None
+    if "fav_gather" in kern and kern["fav_gather"][1]:
+        g_s = kern["fav_gather"][0] / kern["fav_gather"][1] * 1e-3
+        gather_gbs = round(B * n * GATHER_BYTES_PER_KEY / g_s / 1e9, 1)
+    # PCIe-inclusive rate: the host-buffer C-ABI call (bls_fav_batch_indexed: inputs copied H2D, verdicts D2H),
+    # one batch at a time, no pipelining.  Reported beside `value`, never as it.
+    e2e = None
+    if rank == 0 and not args.no_e2e:
+        batch.fast_aggregate_verify_batch(idx, offs, msgs, sigs, ctx=ctx)
+        t1 = time.perf_counter()
+        v2 = batch.fast_aggregate_verify_batch(idx, offs, msgs, sigs, ctx=ctx)
+        e2e = round(B / (time.perf_counter() - t1), 1)
+        assert v2.all()
     total_fme = 11 * n + 14789
     pipeline_ops = (total_fme * FME_OPS + 19 * SHA_OPS) * B * world * args.steps + 9268 * FME_OPS * args.steps
     pipeline_frac = pipeline_ops / dt / (PEAK_INT_OPS * world)
@@ -263,6 +282,8 @@ def main():
         "roofline": roof,
         "int_valu_frac_pipeline": round(pipeline_frac, 5),
         "kernels_avg_ms": kernels_ms,
+        "gather_hbm_gbs": gather_gbs,
+        "host_buffers_fav_s": e2e,
         "device": dev_name, "cus": cus, "setup_s": round(setup_s, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu:

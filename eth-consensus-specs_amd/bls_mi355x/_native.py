@@ -49,6 +49,8 @@ _SIGS = {
     "bls_registry_size": (_sz, [_vp]),
     "bls_fav_batch_indexed": (_ip, [_vp, _vp, _vp, _sz, _u8p, _u8p, _vp]),
     "bls_verify_batch_indexed": (_ip, [_vp, _vp, _sz, _u8p, _u8p, _vp]),
+    "bls_aggregate_verify_batch": (_ip, [_vp, _u8p, _u8p, _vp, _vp, _sz, _u8p, _vp]),
+    "bls_registry_append": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_sign_batch": (_ip, [_vp, _u8p, _u8p, _sz, _vp]),
     "bls_sk_to_pk_batch": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_dev_alloc": (_vp, [_vp, _sz]),

@@ -33,6 +33,12 @@ class Registry:
 
     def __init__(self, ctx: _native.Context | None = None):
         self.ctx = ctx or _native.context()
+        self._index: dict[bytes, int] = {}  # pubkey bytes -> first registry index (host-side lookup)
+
+    def _remember(self, buf: np.ndarray, first: int) -> None:
+        raw = buf.tobytes()
+        for i in range(len(raw) // 48):
+            self._index.setdefault(raw[48 * i: 48 * i + 48], first + i)
 
     def load(self, pubkeys48: bytes | np.ndarray) -> np.ndarray:
         """Decode + KeyValidate ``n`` compressed keys; returns the validity mask."""
@@ -43,7 +49,38 @@ class Registry:
         valid = np.zeros(n, dtype=np.uint8)
         c = self.ctx
         c.check(c.lib.bls_registry_load(c.h, buf.tobytes(), n, _ptr(valid)))
+        self._index = {}
+        self._remember(buf, 0)
         return valid
+
+    def append(self, pubkeys48: bytes | np.ndarray) -> np.ndarray:
+        """Deposits: append keys as validator indices len(self) .. (decode + KeyValidate on the
+        device, existing indices unchanged; specs/phase0/beacon-chain.md:2037-2062).  Returns the
+        validity mask of the new keys."""
+        buf = _u8(pubkeys48)
+        if buf.size % 48:
+            raise ValueError("pubkeys must be a multiple of 48 bytes")
+        n = buf.size // 48
+        first = len(self)
+        valid = np.zeros(n, dtype=np.uint8)
+        c = self.ctx
+        c.check(c.lib.bls_registry_append(c.h, buf.tobytes(), n, _ptr(valid)))
+        self._remember(buf, first)
+        return valid
+
+    def index_of(self, pubkey48: bytes) -> int | None:
+        """Registry index of a compressed pubkey loaded or appended through this object, else None."""
+        return self._index.get(bytes(pubkey48))
+
+    def indices(self, pubkeys) -> np.ndarray | None:
+        """u32 registry indices of every key, or None if any key is not resident."""
+        out = np.empty(len(pubkeys), dtype=np.uint32)
+        for i, pk in enumerate(pubkeys):
+            k = self._index.get(bytes(pk))
+            if k is None:
+                return None
+            out[i] = k
+        return out
 
     def generate(self, n: int, first_sk: int = 1, want_bytes: bool = False):
         """Synthetic registry pk_i = (first_sk + i)*G1 built on the device (benchmarks)."""
@@ -87,6 +124,31 @@ def verify_batch(indices: np.ndarray, msgs32, sigs96, ctx=None) -> np.ndarray:
     out = np.zeros(B, dtype=np.uint8)
     c.check(c.lib.bls_verify_batch_indexed(c.h, _ptr(idx), B, m.tobytes(), s.tobytes(), _ptr(out)))
     return out.astype(bool)
+
+
+def aggregate_verify_batch(pubkeys, messages, signatures, ctx=None) -> np.ndarray:
+    """B AggregateVerify calls -> bool array.  pubkeys[b] / messages[b]: item b's lists of 48-byte keys
+    and messages (any lengths, equal list lengths); signatures[b]: 96 bytes.  An item whose lists differ
+    in length is False (E/utils/bls.py:154-164 returns False on any exception), the rest are checked in
+    one batch (bls_aggregate_verify_batch)."""
+    c = ctx or _native.context()
+    B = len(signatures)
+    if len(pubkeys) != B or len(messages) != B:
+        raise ValueError("need one pubkey list, one message list and one signature per item")
+    good = np.array([len(p) == len(m) and len(bytes(s)) == 96 for p, m, s in zip(pubkeys, messages, signatures)])
+    lens = [len(p) if g else 0 for p, g in zip(pubkeys, good)]
+    io = offsets_from_lengths(lens)
+    flat_pk = [bytes(k) for p, g in zip(pubkeys, good) if g for k in p]
+    if any(len(k) != 48 for k in flat_pk):
+        raise ValueError("pubkeys must be 48 bytes")
+    flat_m = [bytes(m) for ms, g in zip(messages, good) if g for m in ms]
+    mo = offsets_from_lengths([len(m) for m in flat_m])
+    sigs = b"".join(bytes(s) if g else bytes(96) for s, g in zip(signatures, good))
+    out = np.zeros(B, dtype=np.uint8)
+    if B:
+        c.check(c.lib.bls_aggregate_verify_batch(c.h, b"".join(flat_pk), b"".join(flat_m), _ptr(mo), _ptr(io), B,
+                                                 sigs, _ptr(out)))
+    return out.astype(bool) & good
 
 
 def fallback_stats(ctx=None) -> tuple[int, int]:

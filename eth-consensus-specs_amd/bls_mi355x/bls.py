@@ -24,6 +24,10 @@ G2_POINT_AT_INFINITY = b"\xc0" + b"\x00" * 95  # bls.py:80
 # bls.py:81 STUB_COORDINATES = signature_to_G2(G2_POINT_AT_INFINITY): the identity
 STUB_COORDINATES = None
 
+# sigsets.deferred(): when set, the verify family records its arguments here and returns True
+# (the collector checks them all in device batches at the end of the block).
+_collector = None
+
 
 def use_mi355x():
     """Route every BLS call to the MI355X backend (new switch, cf. bls.py:84-121)."""
@@ -72,6 +76,9 @@ def only_with_bls(alt_return=None):  # bls.py:124-138
 
 @only_with_bls(alt_return=True)
 def Verify(PK, message, signature):  # bls.py:141-151
+    if _collector is not None:
+        _collector.add_verify(PK, message, signature)
+        return True
     try:
         result = bls.Verify(PK, message, signature)
     except Exception:
@@ -81,6 +88,9 @@ def Verify(PK, message, signature):  # bls.py:141-151
 
 @only_with_bls(alt_return=True)
 def AggregateVerify(pubkeys, messages, signature):  # bls.py:154-164
+    if _collector is not None:
+        _collector.add_aggregate_verify(pubkeys, messages, signature)
+        return True
     try:
         result = bls.AggregateVerify(list(pubkeys), list(messages), signature)
     except Exception:
@@ -90,6 +100,9 @@ def AggregateVerify(pubkeys, messages, signature):  # bls.py:154-164
 
 @only_with_bls(alt_return=True)
 def FastAggregateVerify(pubkeys, message, signature):  # bls.py:167-177
+    if _collector is not None:
+        _collector.add_fast_aggregate_verify(pubkeys, message, signature)
+        return True
     try:
         result = bls.FastAggregateVerify(list(pubkeys), message, signature)
     except Exception:

@@ -63,6 +63,7 @@ struct bls_ctx {
   G1A* reg = nullptr;
   uint8_t* reg_ok = nullptr;
   size_t reg_n = 0;
+  size_t reg_cap = 0;  // entries allocated (bls_registry_append grows it)
   // per-kernel hipEvent timing of the FAV path (bls_profile_*)
   bool prof_on = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -562,6 +563,7 @@ int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out
   ctx->reg_n = 0;
   HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(G1A)));
   HIPCK(hipMalloc(&ctx->reg_ok, n ? n : 1));
+  ctx->reg_cap = n ? n : 1;
   uint8_t* d_in;
   int* d_ok;
   SCR(S_IN0, 48 * n, d_in);
@@ -572,6 +574,44 @@ int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out
   if (out_valid) CK(d2h(ctx, out_valid, ctx->reg_ok, n));
   HIPCK(hipStreamSynchronize(ctx->j->stream));
   ctx->reg_n = n;
+  return 1;
+}
+
+int bls_registry_append(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid) {
+  API_ENTER(ctx);
+  if (!pks48 && n) return BLS_E_ARG;
+  if (ctx->reg_n + n > 0xffffffffu) return BLS_E_ARG;
+  if (n == 0) return 1;
+  const size_t need = ctx->reg_n + n;
+  if (need > ctx->reg_cap) {  // grow by >= 1/4 so a run of deposits reallocates rarely
+    HIPCK(hipDeviceSynchronize());  // batches in flight on any job read the old table
+    size_t cap = ctx->reg_cap + ctx->reg_cap / 4;
+    if (cap < need) cap = need;
+    G1A* nreg;
+    uint8_t* nok;
+    HIPCK(hipMalloc(&nreg, cap * sizeof(G1A)));
+    HIPCK(hipMalloc(&nok, cap));
+    if (ctx->reg_n) {
+      HIPCK(hipMemcpyAsync(nreg, ctx->reg, ctx->reg_n * sizeof(G1A), hipMemcpyDeviceToDevice, ctx->j->stream));
+      HIPCK(hipMemcpyAsync(nok, ctx->reg_ok, ctx->reg_n, hipMemcpyDeviceToDevice, ctx->j->stream));
+      HIPCK(hipStreamSynchronize(ctx->j->stream));
+    }
+    if (ctx->reg) HIPCK(hipFree(ctx->reg));
+    if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
+    ctx->reg = nreg;
+    ctx->reg_ok = nok;
+    ctx->reg_cap = cap;
+  }
+  uint8_t* d_in;
+  int* d_ok;
+  SCR(S_IN0, 48 * n, d_in);
+  SCR(S_OK, n, d_ok);
+  CK(h2d(ctx, d_in, pks48, 48 * n));
+  LK(launch_key_validate(ctx->j->stream, d_in, n, ctx->reg + ctx->reg_n, d_ok));
+  LK(launch_status_to_u8(ctx->j->stream, d_ok, n, ctx->reg_ok + ctx->reg_n));
+  if (out_valid) CK(d2h(ctx, out_valid, ctx->reg_ok + ctx->reg_n, n));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  ctx->reg_n = need;
   return 1;
 }
 
@@ -588,6 +628,7 @@ int bls_registry_generate(bls_ctx* ctx, uint64_t first_sk, size_t n, uint8_t* ou
   ctx->reg_n = 0;
   HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(G1A)));
   HIPCK(hipMalloc(&ctx->reg_ok, n ? n : 1));
+  ctx->reg_cap = n ? n : 1;
   G1J* tmp;
   uint8_t* d_out = nullptr;
   SCR(S_G1J_T, n, tmp);
@@ -855,6 +896,113 @@ int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const 
   std::vector<uint64_t> offs(B + 1);
   for (size_t i = 0; i <= B; i++) offs[i] = i;
   return fav_batch_host(ctx, idx, offs.data(), B, msgs32, sigs96, out);
+}
+
+int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t* msgs, const uint64_t* msg_offs,
+                               const uint64_t* item_offs, size_t B, const uint8_t* sigs96, uint8_t* out) {
+  API_ENTER(ctx);
+  if ((B && (!item_offs || !sigs96 || !out)) || B > 0xffffffffu) return BLS_E_ARG;
+  if (B == 0) return 1;
+  if (item_offs[0] != 0) return BLS_E_ARG;
+  for (size_t b = 0; b < B; b++)
+    if (item_offs[b + 1] < item_offs[b]) return BLS_E_ARG;
+  const size_t total = item_offs[B];
+  if (total && (!pks48 || !msg_offs)) return BLS_E_ARG;
+  if (total > 0xffffffffu) return BLS_E_ARG;
+  if (total) {
+    if (msg_offs[0] != 0) return BLS_E_ARG;
+    for (size_t t = 0; t < total; t++)
+      if (msg_offs[t + 1] < msg_offs[t] || msg_offs[t + 1] - msg_offs[t] > 0xffffffffu) return BLS_E_ARG;
+    if (msg_offs[total] && !msgs) return BLS_E_ARG;
+  }
+  ctx->j->bis_checks = ctx->j->bis_rounds = 0;
+  hipStream_t st = ctx->j->stream;
+  const size_t npair = total + B;
+  // inputs
+  uint8_t *d_pk, *d_sig, *d_msgs;
+  uint64_t *d_moffs, *d_io, *d_rsc;
+  uint32_t* d_pitem;
+  SCR(S_IN0, 48 * total, d_pk);
+  SCR(S_IN1, 96 * B, d_sig);
+  SCR(S_IN2, total ? msg_offs[total] : 0, d_msgs);
+  SCR(S_OFFS, total + 1, d_moffs);
+  SCR(S_IN3, B + 1, d_io);
+  SCR(S_RSC, B, d_rsc);
+  SCR(S_BSEL, total, d_pitem);
+  std::vector<uint32_t> pitem(total);
+  for (size_t b = 0; b < B; b++)
+    for (uint64_t t = item_offs[b]; t < item_offs[b + 1]; t++) pitem[t] = (uint32_t)b;
+  std::vector<uint64_t> rsc(B);
+  {
+    uint8_t seed[32];
+    host_seed(seed);
+    uint64_t x = 0, y = 0;
+    memcpy(&x, seed, 8);
+    memcpy(&y, seed + 8, 8);
+    for (size_t b = 0; b < B; b++) {  // splitmix64 stream keyed by the OS seed; r_b != 0
+      x += 0x9e3779b97f4a7c15ull;
+      uint64_t z = x ^ y;
+      z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+      z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+      z ^= z >> 31;
+      rsc[b] = z ? z : 1;
+    }
+  }
+  CK(h2d(ctx, d_pk, pks48, 48 * total));
+  CK(h2d(ctx, d_sig, sigs96, 96 * B));
+  if (total) {
+    CK(h2d(ctx, d_msgs, msgs, msg_offs[total]));
+    CK(h2d(ctx, d_moffs, msg_offs, (total + 1) * sizeof(uint64_t)));
+  }
+  CK(h2d(ctx, d_io, item_offs, (B + 1) * sizeof(uint64_t)));
+  CK(h2d(ctx, d_rsc, rsc.data(), B * sizeof(uint64_t)));
+  CK(h2d(ctx, d_pitem, pitem.data(), total * sizeof(uint32_t)));
+  // per-key / per-signature validation, hash_to_G2 of every message
+  G1A *d_pa, *P2;
+  G2A *d_sa, *d_h, *Q2;
+  int *d_pok, *d_sok, *d_status, *d_res;
+  Fp12 *f, *ft, *fo, *fi;
+  SCR(S_G1A, total, d_pa);
+  SCR(S_OK, total, d_pok);
+  SCR(S_SIG, B, d_sa);
+  SCR(S_MSTAT, B, d_sok);
+  SCR(S_H, total, d_h);
+  SCR(S_STATUS, B, d_status);
+  SCR(S_BP, npair, P2);
+  SCR(S_BQ, npair, Q2);
+  SCR(S_F, npair, f);
+  SCR(S_F_T, npair / 8 + 16, ft);
+  SCR(S_FPART, 1, fo);
+  LK(launch_key_validate(st, d_pk, total, d_pa, d_pok));
+  LK(launch_sig_validate(st, d_sig, B, d_sa, d_sok));
+  LK(launch_hash_many(st, d_msgs, d_moffs, total, nullptr, 0, d_h));
+  LK(launch_av_items(st, B, d_io, d_pok, d_sok, d_sa, d_rsc, d_status, P2, Q2));
+  LK(launch_av_pairs(st, total, d_pitem, d_status, d_rsc, d_pa, d_h, P2, Q2));
+  PROF(5, launch_miller_wave(st, P2, Q2, nullptr, npair, f));
+  PROF(6, launch_fp12_prod_vm(st, f, npair, ft, fo));
+  std::vector<int> status(B);
+  CK(d2h(ctx, status.data(), d_status, B * sizeof(int)));
+  const int batch_ok = run_final_check(ctx, fo);
+  if (batch_ok < 0) return batch_ok;
+  if (!batch_ok) {  // each item on its own: its segment of Miller values, one final exponentiation each
+    std::vector<uint32_t> sel;
+    for (size_t b = 0; b < B; b++)
+      if (status[b]) sel.push_back((uint32_t)b);
+    uint32_t* d_sel;
+    SCR(S_BBAD, sel.size(), d_sel);
+    SCR(S_BT, B, fi);
+    SCR(S_BRES, sel.size(), d_res);
+    CK(h2d(ctx, d_sel, sel.data(), sel.size() * sizeof(uint32_t)));
+    LK(launch_fp12_seg_prod(st, f, d_io, B, fi));
+    LK(launch_final_check_sel(st, fi, d_sel, sel.size(), d_res));
+    std::vector<int> res(sel.size());
+    CK(d2h(ctx, res.data(), d_res, sel.size() * sizeof(int)));
+    for (size_t k = 0; k < sel.size(); k++) status[sel[k]] = res[k];
+    ctx->j->bis_checks = sel.size();
+    ctx->j->bis_rounds = 1;
+  }
+  for (size_t b = 0; b < B; b++) out[b] = status[b] ? 1 : 0;
+  return 1;
 }
 
 int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds) {

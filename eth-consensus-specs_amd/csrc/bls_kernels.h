@@ -17,6 +17,10 @@ hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* m
 hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok);
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status);
 hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP, const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2);
+hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok, const G2A* sig, const uint64_t* rsc, int* status, G1A* P2, G2A* Q2);
+hipError_t launch_av_pairs(hipStream_t st, size_t total, const uint32_t* pair_item, const int* status, const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2);
+// out[b] = product of in[io[b] + b .. io[b + 1] + b] (the AggregateVerify batch's per-item segments)
+hipError_t launch_fp12_seg_prod(hipStream_t st, const Fp12* in, const uint64_t* io, size_t B, Fp12* out);
 hipError_t launch_verdicts(hipStream_t st, const int* status, const uint8_t* bad, size_t B, uint8_t* out);
 hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out);
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out);

@@ -2,6 +2,8 @@
 // (verification, key, signature, pair) unless noted; reductions (aggregate
 // pubkeys, sum of r_i*sig_i, Miller-product) are LDS trees inside a
 // workgroup followed by a second pass over the per-workgroup partials.
+#include <cstdlib>
+
 #include "bls_kernels.h"
 
 namespace bls {
@@ -222,35 +224,46 @@ __device__ __forceinline__ G1P g1p_add(const G1P& p, const G1P& q) {
   return r;
 }
 
+// L lanes per aggregate, 64 / L aggregates per workgroup.  The LDS tree
+// costs log2(L) full additions of the whole wave, so for mainnet-sized
+// committees L = 16 (32 mixed additions per lane + 4 tree levels) beats 64
+// lanes (8 + 6 levels: the tree was ~45 % of the wave's time).
+template <int L>
 __global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
                                                    const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status) {
+  constexpr int IPW = 64 / L;
   __shared__ G1P sh[64];
-  __shared__ int bad;
-  const size_t b = blockIdx.x;
-  if (b >= B) return;
-  if (threadIdx.x == 0) bad = 0;
+  __shared__ int bad[IPW];
+  const int sub = (int)threadIdx.x / L, ln = (int)threadIdx.x % L;
+  const size_t b = (size_t)blockIdx.x * IPW + sub;
+  if ((int)threadIdx.x < IPW) bad[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t lo = offs[b], hi = offs[b + 1];
   G1P acc{fp_zero(), FP_ONE, fp_zero()};  // identity (0 : 1 : 0)
   int mybad = 0;
-  for (uint64_t j = lo + threadIdx.x; j < hi; j += 64) {
-    const uint32_t k = idx[j];
-    if (k >= reg_n || !reg_ok[k]) {
-      mybad = 1;
-    } else {
-      acc = g1p_add_aff(acc, reg[k].x, reg[k].y);
+  uint64_t lo = 0, hi = 0;
+  if (b < B) {
+    lo = offs[b];
+    hi = offs[b + 1];
+    for (uint64_t j = lo + ln; j < hi; j += L) {
+      const uint32_t k = idx[j];
+      if (k >= reg_n || !reg_ok[k]) {
+        mybad = 1;
+      } else {
+        acc = g1p_add_aff(acc, reg[k].x, reg[k].y);
+      }
     }
   }
-  if (mybad) atomicOr(&bad, 1);
+  if (mybad) atomicOr(&bad[sub], 1);
   sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int s = 32; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) sh[threadIdx.x] = g1p_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+#pragma unroll 1
+  for (int s = L / 2; s > 0; s >>= 1) {
+    if (ln < s) sh[threadIdx.x] = g1p_add(sh[threadIdx.x], sh[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) {  // projective aggregate key; the identity is invalid (KeyValidate of the sum)
-    apk[b] = sh[0];
-    status[b] = (hi > lo && !bad && !fp_is_zero(sh[0].z)) ? 1 : 0;
+  if (ln == 0 && b < B) {  // projective aggregate key; the identity is invalid (KeyValidate of the sum)
+    apk[b] = sh[threadIdx.x];
+    status[b] = (hi > lo && !bad[sub] && !fp_is_zero(sh[threadIdx.x].z)) ? 1 : 0;
   }
 }
 
@@ -277,6 +290,43 @@ __global__ void __launch_bounds__(64) k_bisect_pairs(size_t B, const uint64_t* r
   Q2[2 * i + 1] = sig[i];
   st2[2 * i] = st;
   st2[2 * i + 1] = st;
+}
+
+// (5) AggregateVerify batches (bls_aggregate_verify_batch).  Item b owns the
+//     n_b pairs (pk_bj, m_bj) at pair indices io[b] .. io[b+1] and one
+//     signature; its pairs are laid out at io[b] + b + j, followed by the
+//     signature pair at io[b+1] + b.  With a random 64-bit r_b per item the
+//     item's pairs are (r_b pk_bj, H(m_bj)) and (-r_b G1, sigma_b): their
+//     Miller product is the item's check raised to r_b, so the product over
+//     all items is the batch's random-linear-combination check and any
+//     item's own segment is its individual check (fallback).
+__global__ void __launch_bounds__(64) k_av_items(size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok,
+                                                 const G2A* sig, const uint64_t* rsc, int* status, G1A* P2, G2A* Q2) {
+  const size_t b = gtid();
+  if (b >= B) return;
+  const uint64_t lo = io[b], hi = io[b + 1];
+  int st = hi > lo && sig_ok[b];
+  for (uint64_t j = lo; st && j < hi; j++) st = pk_ok[j] != 0;
+  status[b] = st;
+  G1A ng{fp_zero(), fp_zero(), true};
+  if (st) {
+    G1A g = g1_generator();
+    g.y = fp_neg(g.y);
+    ng = jac_to_aff(jac_mul_u64(jac_from_aff(g), rsc[b]));
+  }
+  P2[hi + b] = ng;
+  Q2[hi + b] = sig[b];
+}
+
+__global__ void __launch_bounds__(64) k_av_pairs(size_t total, const uint32_t* pair_item, const int* status,
+                                                 const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2) {
+  const size_t t = gtid();
+  if (t >= total) return;
+  const uint32_t b = pair_item[t];
+  G1A rp{fp_zero(), fp_zero(), true};
+  if (status[b]) rp = jac_to_aff(jac_mul_u64(jac_from_aff(pk[t]), rsc[b]));
+  P2[t + b] = rp;
+  Q2[t + b] = H[t];
 }
 
 // Verdicts: valid iff the per-item checks passed and bisection did not isolate it.
@@ -423,13 +473,36 @@ hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, ui
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
                              const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status) {
   if (!B) return hipSuccess;
-  LAUNCH(k_fav_gather, (unsigned)B, 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+  // lanes per aggregate: 16 while that still gives >= ~2 waves per SIMD and the
+  // committees are not huge (the per-lane chains stay short), else 64
+  static const int forced = getenv("BLS_GATHER_L") ? atoi(getenv("BLS_GATHER_L")) : 0;
+  int L = forced ? forced : (B >= 8192 ? 16 : 64);
+  if (L == 16)
+    LAUNCH(k_fav_gather<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+  else if (L == 8)
+    LAUNCH(k_fav_gather<8>, (unsigned)((B + 7) / 8), 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+  else if (L == 32)
+    LAUNCH(k_fav_gather<32>, (unsigned)((B + 1) / 2), 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+  else
+    LAUNCH(k_fav_gather<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
   return hipSuccess;
 }
 hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP,
                                const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2) {
   if (!B) return hipSuccess;
   LAUNCH(k_bisect_pairs, nblk(B, 64), 64, st, B, rsc, status, rP, H, sig, P2, Q2, st2);
+  return hipSuccess;
+}
+hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok,
+                           const G2A* sig, const uint64_t* rsc, int* status, G1A* P2, G2A* Q2) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_av_items, nblk(B, 64), 64, st, B, io, pk_ok, sig_ok, sig, rsc, status, P2, Q2);
+  return hipSuccess;
+}
+hipError_t launch_av_pairs(hipStream_t st, size_t total, const uint32_t* pair_item, const int* status,
+                           const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2) {
+  if (!total) return hipSuccess;
+  LAUNCH(k_av_pairs, nblk(total, 64), 64, st, total, pair_item, status, rsc, pk, H, P2, Q2);
   return hipSuccess;
 }
 hipError_t launch_verdicts(hipStream_t st, const int* status, const uint8_t* bad, size_t B, uint8_t* out) {

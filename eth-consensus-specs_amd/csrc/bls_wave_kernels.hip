@@ -240,6 +240,27 @@ __global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n
   if (threadIdx.x < 12) fp12_slot_dst(outp[blockIdx.x], threadIdx.x) = fp_from_fd(s[base + threadIdx.x]);
 }
 
+// Ragged segments: out[b] = prod in[io[b] + b .. io[b + 1] + b] (inclusive).
+__global__ void __launch_bounds__(64) k_fp12_seg_prod(const Fp12* in, const uint64_t* io, size_t B, Fp12* outp) {
+  __shared__ Fd s[WP_NCONST + WL_CH_STRIDE];
+  const size_t b = blockIdx.x;
+  const size_t lo = io[b] + b, hi = io[b + 1] + b + 1;
+  vm_load_consts(s);
+  const int base = WP_NCONST;
+  load_fp12(s + base, in + lo);
+  for (size_t i = lo + 1; i < hi; i++) {
+    load_fp12(s + base + 12, in + i);
+    vm_run<1>(VM_PROG(CH_MUL), s, base, 0, nullptr);
+  }
+  if (threadIdx.x < 12) fp12_slot_dst(outp[b], threadIdx.x) = fp_from_fd(s[base + threadIdx.x]);
+}
+
+hipError_t launch_fp12_seg_prod(hipStream_t st, const Fp12* in, const uint64_t* io, size_t B, Fp12* out) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_seg_prod, dim3((unsigned)B), dim3(64), 0, st, in, io, B, out);
+  return hipGetLastError();
+}
+
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;

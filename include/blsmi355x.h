@@ -106,6 +106,25 @@ int bls_fav_batch_indexed(bls_ctx* ctx, const uint32_t* idx, const uint64_t* off
 int bls_verify_batch_indexed(bls_ctx* ctx, const uint32_t* idx, size_t B, const uint8_t* msgs32,
                              const uint8_t* sigs96, uint8_t* out);
 
+/* B AggregateVerify calls  <- E/utils/bls.py:154-164 (one call per item).
+ * Item b owns the pairs item_offs[b] .. item_offs[b+1] (item_offs has B+1
+ * entries, total = item_offs[B]): pubkeys pks48[48 t ..], messages
+ * msgs[msg_offs[t] .. msg_offs[t+1]) (msg_offs has total+1 entries, any
+ * lengths), and signature sigs96[96 b ..].  out[b] = 1/0 with the per-call
+ * semantics of bls_aggregate_verify (empty item, invalid key or signature ->
+ * 0).  One random-linear-combination pairing check over all items; when it
+ * fails every item is checked on its own (batched final exponentiations).
+ * Returns 1 or BLS_E_*. */
+int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t* msgs, const uint64_t* msg_offs,
+                               const uint64_t* item_offs, size_t B, const uint8_t* sigs96, uint8_t* out);
+
+/* Append n compressed keys to the HBM registry (deposits: new validator
+ * indices reg_n .. reg_n + n), decoding + KeyValidate on the device like
+ * bls_registry_load; out_valid as there.  Existing entries keep their
+ * indices.  <- specs/phase0/beacon-chain.md:2037-2062 (add_validator_to_registry),
+ * specs/electra/beacon-chain.md:1577-1588.  Returns 1 or BLS_E_*. */
+int bls_registry_append(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid);
+
 /* Fallback statistics of the last batch call on this context: the number of
  * batched final-exponentiation checks and bisection rounds it ran (both 0
  * when the whole-batch check passed).  Returns 0 or BLS_E_*. */
