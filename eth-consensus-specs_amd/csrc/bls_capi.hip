@@ -22,6 +22,9 @@ enum Slot {
   S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
+  // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
+  S_AV_IO, S_AV_RSC, S_AV_PITEM, S_AV_SIG, S_AV_SOK, S_AV_H, S_AV_ST, S_AV_P, S_AV_Q, S_AV_F, S_AV_FT, S_AV_SEL,
+  S_AV_FI, S_AV_RES, S_AV_U, S_AV_HCF, S_AV_FLAG,
   NSLOT
 };
 
@@ -395,7 +398,15 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   if (!sok) return 0;
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
-  LK(launch_hash_many(ctx->j->stream, d_msgs, d_offs, n, nullptr, 0, Q));
+  {
+    Fp* d_u;
+    Fd* d_hf;
+    int* d_flag;
+    SCR(S_AV_U, 8 * n, d_u);
+    SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
+    SCR(S_AV_FLAG, n, d_flag);
+    LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_u, d_hf, Q, d_flag));
+  }
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->j->stream, P + n);
   LK(hipGetLastError());
   LK(launch_miller_wave(ctx->j->stream, P, Q, nullptr, n + 1, f));
@@ -926,9 +937,9 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
   SCR(S_IN1, 96 * B, d_sig);
   SCR(S_IN2, total ? msg_offs[total] : 0, d_msgs);
   SCR(S_OFFS, total + 1, d_moffs);
-  SCR(S_IN3, B + 1, d_io);
-  SCR(S_RSC, B, d_rsc);
-  SCR(S_BSEL, total, d_pitem);
+  SCR(S_AV_IO, B + 1, d_io);
+  SCR(S_AV_RSC, B, d_rsc);
+  SCR(S_AV_PITEM, total, d_pitem);
   std::vector<uint32_t> pitem(total);
   for (size_t b = 0; b < B; b++)
     for (uint64_t t = item_offs[b]; t < item_offs[b + 1]; t++) pitem[t] = (uint32_t)b;
@@ -964,18 +975,26 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
   Fp12 *f, *ft, *fo, *fi;
   SCR(S_G1A, total, d_pa);
   SCR(S_OK, total, d_pok);
-  SCR(S_SIG, B, d_sa);
-  SCR(S_MSTAT, B, d_sok);
-  SCR(S_H, total, d_h);
-  SCR(S_STATUS, B, d_status);
-  SCR(S_BP, npair, P2);
-  SCR(S_BQ, npair, Q2);
-  SCR(S_F, npair, f);
-  SCR(S_F_T, npair / 8 + 16, ft);
+  SCR(S_AV_SIG, B, d_sa);
+  SCR(S_AV_SOK, B, d_sok);
+  SCR(S_AV_H, total, d_h);
+  SCR(S_AV_ST, B, d_status);
+  SCR(S_AV_P, npair, P2);
+  SCR(S_AV_Q, npair, Q2);
+  SCR(S_AV_F, npair, f);
+  SCR(S_AV_FT, npair / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   LK(launch_key_validate(st, d_pk, total, d_pa, d_pok));
   LK(launch_sig_validate(st, d_sig, B, d_sa, d_sok));
-  LK(launch_hash_many(st, d_msgs, d_moffs, total, nullptr, 0, d_h));
+  {  // hash_to_G2 of every message: lane SSWU + VM isogeny / cofactor clearing (as in the FAV batch)
+    Fp* d_u;
+    Fd* d_hf;
+    int* d_flag;
+    SCR(S_AV_U, 8 * total, d_u);
+    SCR(S_AV_HCF, h2c_scratch_fd(total), d_hf);
+    SCR(S_AV_FLAG, total, d_flag);
+    LK(launch_h2c_msgs(st, total, d_msgs, d_moffs, d_u, d_hf, d_h, d_flag));
+  }
   LK(launch_av_items(st, B, d_io, d_pok, d_sok, d_sa, d_rsc, d_status, P2, Q2));
   LK(launch_av_pairs(st, total, d_pitem, d_status, d_rsc, d_pa, d_h, P2, Q2));
   PROF(5, launch_miller_wave(st, P2, Q2, nullptr, npair, f));
@@ -989,9 +1008,9 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
     for (size_t b = 0; b < B; b++)
       if (status[b]) sel.push_back((uint32_t)b);
     uint32_t* d_sel;
-    SCR(S_BBAD, sel.size(), d_sel);
-    SCR(S_BT, B, fi);
-    SCR(S_BRES, sel.size(), d_res);
+    SCR(S_AV_SEL, sel.size(), d_sel);
+    SCR(S_AV_FI, B, fi);
+    SCR(S_AV_RES, sel.size(), d_res);
     CK(h2d(ctx, d_sel, sel.data(), sel.size() * sizeof(uint32_t)));
     LK(launch_fp12_seg_prod(st, f, d_io, B, fi));
     LK(launch_final_check_sel(st, fi, d_sel, sel.size(), d_res));

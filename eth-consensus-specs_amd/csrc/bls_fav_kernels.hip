@@ -41,6 +41,23 @@ __global__ void __launch_bounds__(64) k_h2c_sswu(size_t B, const uint8_t* msgs32
   o[3] = y.c1;
 }
 
+// Messages of any length (AggregateVerify): item i is msgs[offs[i] .. offs[i+1]).
+__global__ void __launch_bounds__(64) k_h2c_sswu_var(size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U) {
+  const size_t k = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = k >> 1;
+  const int t = (int)(k & 1);
+  if (i >= B) return;
+  Fp2 u[2];
+  hash_to_field_fp2(u, msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_FAV, 43);
+  Fp2 x, y;
+  map_to_curve_sswu_lane(x, y, u[t]);
+  Fp* o = U + 8 * i + 4 * t;
+  o[0] = x.c0;
+  o[1] = x.c1;
+  o[2] = y.c0;
+  o[3] = y.c1;
+}
+
 // (2) isogeny, sum, cofactor clearing and affine conversion on the VM, in
 // phases (HBM staging in Fd form, 24 slots per item: Q | M | A | C):
 //   k_h2c_iso    U -> Q = iso(U0) + iso(U1), flag
@@ -181,6 +198,13 @@ __global__ void __launch_bounds__(64) k_h2c_fallback(size_t B, const uint8_t* ms
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B || !flag[i]) return;
   H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_FAV, 43));
+}
+
+__global__ void __launch_bounds__(64) k_h2c_fallback_var(size_t B, const uint8_t* msgs, const uint64_t* offs,
+                                                         const int* flag, G2A* H) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || !flag[i]) return;
+  H[i] = jac_to_aff(hash_to_g2(msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_FAV, 43));
 }
 
 // ----------------------------------------------------------- signatures --
@@ -333,6 +357,18 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
               : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_h2c_fallback, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, flag, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U, Fd* hf,
+                           G2A* H, int* flag) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_h2c_sswu_var, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, U);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, 5);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_h2c_fallback_var, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs, offs, flag, H);
   return hipGetLastError();
 }
 

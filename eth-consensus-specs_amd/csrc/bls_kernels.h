@@ -32,6 +32,9 @@ hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const 
 size_t h2c_scratch_fd(size_t B);
 hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
                       int* flag);
+// hash_to_G2 (POP DST) of B messages of any length, msgs[offs[i] .. offs[i+1]); same phases as launch_h2c
+hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U, Fd* hf, G2A* H,
+                           int* flag);
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat);
 // rPj: B projective scratch points (r_i apk_i before the affine conversion)
 hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff, const G2A* sig,
