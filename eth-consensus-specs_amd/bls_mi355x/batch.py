@@ -17,7 +17,9 @@ import numpy as np
 
 from . import _native
 
-FAV_JOBS = 4  # BLS_FAV_JOBS in include/blsmi355x.h: batches in flight on one context
+FAV_JOBS = 4  # BLS_FAV_JOBS in include/blsmi355x.h: per-context job slots
+# batches kept in flight by run_pipelined (<= FAV_JOBS)
+FAV_DEPTH = max(1, min(FAV_JOBS, int(os.environ.get("BLS_FAV_DEPTH", "4"))))
 
 
 def _ptr(a: np.ndarray):
@@ -261,7 +263,7 @@ class ResidentFavBatch:
         c.check(c.lib.bls_fav_job_finish_dev(c.h, job, 1 if batch_ok else 0, self.outs[job].ptr))
         self.last_job = job
 
-    def run_pipelined(self, seeds, exchange=None, depth: int = FAV_JOBS) -> list:
+    def run_pipelined(self, seeds, exchange=None, depth: int = FAV_DEPTH) -> list:
         """One pass over the batch per seed with up to `depth` passes in flight:
         pass k+1.. are submitted before pass k is final-exponentiated (their
         front kernels overlap pass k's tail).  exchange(partial) -> concatenated

@@ -244,6 +244,17 @@ struct JobScope {
   if ((job) < 0 || (job) >= BLS_FAV_JOBS) return BLS_E_ARG;  \
   JobScope job_scope_(ctx, job)
 
+// Hardware-queue policy (see bls_mi355x/_native.py hw_queue_policy): the
+// FAV pipeline keeps BLS_FAV_JOBS x 3 streams busy, and with HIP's default of
+// 4 hardware queues a long lane kernel blocks the streams sharing its queue.
+// Applied when the library is loaded, i.e. before this library's first HIP
+// call; a host that initialised HIP earlier keeps its own setting.
+__attribute__((constructor)) static void bls_hw_queue_policy() {
+  if (getenv("BLSMI355X_KEEP_HW_QUEUES")) return;
+  const char* v = getenv("GPU_MAX_HW_QUEUES");
+  if (!v || atoi(v) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+}
+
 extern "C" {
 
 static bool job_init(Job& J, int prio_hi) {
@@ -746,8 +757,14 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   PROF(10, launch_sig_vm(st, B, status, dstat, apka, sig, rsc, rpj, rP));
   // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_join, 0));
-  PROF(5, launch_miller2(st, rP, H, status, B, f));
-  PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
+  static const bool ml_vm = getenv("BLS_ML_VM") != nullptr;  // A/B knob: wave-program Miller (2 pairs per f)
+  if (ml_vm) {
+    PROF(5, launch_miller2(st, rP, H, status, B, f));
+    PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
+  } else {
+    PROF(5, launch_miller_lane(st, rP, H, status, B, f));
+    PROF(6, launch_fp12_prod_vm(st, f, B, ft, f + B));
+  }
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_msm, 0));
   LK(launch_fp12_prod_vm(st, f + B, 2, ft, fo));
   ctx->j->fav_B = B;

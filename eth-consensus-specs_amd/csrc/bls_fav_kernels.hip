@@ -70,7 +70,6 @@ __global__ void __launch_bounds__(64) k_h2c_sswu_var(size_t B, const uint8_t* ms
 // 5 items share a workgroup instead of 2.
 // flag[i] = 1 when an isogeny denominator vanished (the item is recomputed
 // by k_h2c_fallback; unreachable for SHA-256 outputs in practice).
-constexpr int HCF = 24;  // staged Fd slots per item
 constexpr int HCF_Q = 0, HCF_M = 6, HCF_A = 12, HCF_C = 18;
 
 template <int G>
@@ -332,7 +331,10 @@ static hipError_t launch_h2c_phases(hipStream_t st, size_t B, const int* status,
   hipLaunchKernelGGL(k_h2c_iso<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, U, hf, flag);
   for (int pass = 0; pass < 2; pass++) {  // M = [|x|] Q, then M = [|x|] A
     const int src = pass ? HCF_A : HCF_Q;
-    if (xg == 4)
+    if (xg == 1) {  // default: one lane per item (bls_chain_lane.hip)
+      hipError_t e = launch_g2x_lane(st, B, hf, src, HCF_M);
+      if (e != hipSuccess) return e;
+    } else if (xg == 4)
       hipLaunchKernelGGL(k_g2x_chain<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, hf, src, HCF_M);
     else if (xg == 6)
       hipLaunchKernelGGL(k_g2x_chain<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, hf, src, HCF_M);
@@ -352,7 +354,7 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   static const int hg = env_g("BLS_H2C_G", 2);  // tuning knobs: items per workgroup
-  static const int xg = env_int_or("BLS_XC_G", 5);
+  static const int xg = env_int_or("BLS_XC_G", 5);  // 4/5/6: wave programs (default: shorter h2c latency); 1: lane chains
   e = hg == 4 ? launch_h2c_phases<4>(st, B, status, U, hf, H, flag, xg)
               : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
   if (e != hipSuccess) return e;
@@ -366,7 +368,7 @@ hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const 
   hipLaunchKernelGGL(k_h2c_sswu_var, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, 5);
+  e = launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, env_int_or("BLS_XC_G", 5));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_h2c_fallback_var, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs, offs, flag, H);
   return hipGetLastError();
@@ -382,8 +384,11 @@ hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, co
 hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff,
                          const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP) {
   if (!B) return hipSuccess;
-  static const int sg = env_g("BLS_SIG_G", 4);  // tuning knob: items per workgroup
-  if (sg == 4)
+  static const int sg = env_int_or("BLS_SIG_G", 1);  // 1: one lane per item; 2/4/6: wave programs
+  if (sg == 1) {
+    hipError_t e = launch_sig_lane(st, B, status, dstat, apk_aff, sig, rsc, rPj);
+    if (e != hipSuccess) return e;
+  } else if (sg == 4)
     hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
   else if (sg == 6)
     hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);

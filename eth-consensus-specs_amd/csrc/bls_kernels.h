@@ -28,6 +28,11 @@ hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, F
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96);
 hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok, uint8_t* out48);
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
+constexpr int HCF = 24;  // hash_to_G2 staging: Fd slots per item (bls_fav_kernels.hip, bls_chain_lane.hip)
+// one lane per item (bls_chain_lane.hip)
+hipError_t launch_sig_lane(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk, const G2A* sig,
+                           const uint64_t* rsc, G1P* rPj);
+hipError_t launch_g2x_lane(hipStream_t st, size_t B, Fd* hf, int src, int dst);
 // hf: h2c_scratch_fd(B) Fd slots of staging between the hash_to_G2 phases
 size_t h2c_scratch_fd(size_t B);
 hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
@@ -42,6 +47,8 @@ hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat
 size_t msm_scratch_u32(size_t B);
 size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
+// one lane per pair (bls_miller_lane.hip): f[i] = Miller value of pair i (1 if skipped)
+hipError_t launch_miller_lane(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
 // nsel independent checks: out[b] = (FE(f[sel[b]]) == 1)
