@@ -72,6 +72,10 @@ _SIGS = {
     "bls_verify_batch_indexed": (_ip, [_vp, _vp, _sz, _u8p, _u8p, _vp]),
     "bls_aggregate_verify_batch": (_ip, [_vp, _u8p, _u8p, _vp, _vp, _sz, _u8p, _vp]),
     "bls_registry_append": (_ip, [_vp, _u8p, _sz, _vp]),
+    "bls_signing_roots": (_ip, [_vp, _u8p, _u8p, _sz, _sz, _vp]),
+    "bls_merkleize": (_ip, [_vp, _u8p, _sz, _ip, _vp]),
+    "bls_pairing_check": (_ip, [_vp, _u8p, _u8p, _sz]),
+    "bls_g1_multi_exp": (_ip, [_vp, _u8p, _u8p, _sz, _vp]),
     "bls_sign_batch": (_ip, [_vp, _u8p, _u8p, _sz, _vp]),
     "bls_sk_to_pk_batch": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_dev_alloc": (_vp, [_vp, _sz]),

@@ -153,6 +153,78 @@ def aggregate_verify_batch(pubkeys, messages, signatures, ctx=None) -> np.ndarra
     return out.astype(bool) & good
 
 
+def compute_signing_roots(object_roots, domains, ctx=None) -> list[bytes]:
+    """compute_signing_root for many objects on the device (specs/phase0/beacon-chain.md:953-962):
+    SHA-256(object_root || domain).  ``domains``: one 32-byte domain for all, or one per root."""
+    c = ctx or _native.context()
+    roots = [bytes(r) for r in object_roots]
+    if any(len(r) != 32 for r in roots):
+        raise ValueError("object roots must be 32 bytes")
+    if isinstance(domains, (bytes, bytearray)) and len(domains) == 32:
+        dom, stride = bytes(domains), 0
+    else:
+        dl = [bytes(d) for d in domains]
+        if len(dl) != len(roots) or any(len(d) != 32 for d in dl):
+            raise ValueError("need one 32-byte domain, or one per root")
+        dom, stride = b"".join(dl), 32
+    n = len(roots)
+    out = ctypes.create_string_buffer(32 * n) if n else None
+    c.check(c.lib.bls_signing_roots(c.h, b"".join(roots), dom, stride, n, out))
+    return [out.raw[32 * i: 32 * i + 32] for i in range(n)]
+
+
+def merkleize(chunks, limit: int | None = None, ctx=None) -> bytes:
+    """SSZ merkleize(chunks, limit) on the device: the tree has next_pow2(limit or len(chunks)) leaves."""
+    c = ctx or _native.context()
+    ch = [bytes(x) for x in chunks]
+    if any(len(x) != 32 for x in ch):
+        raise ValueError("chunks must be 32 bytes")
+    n = len(ch)
+    size = n if limit is None else limit
+    if size < n:
+        raise ValueError("more chunks than the limit")
+    depth = max(size - 1, 0).bit_length()
+    out = ctypes.create_string_buffer(32)
+    c.check(c.lib.bls_merkleize(c.h, b"".join(ch) if n else None, n, depth, out))
+    return out.raw
+
+
+def mix_in_length(root: bytes, length: int) -> bytes:
+    """hash_tree_root of a list: SHA-256(root || uint256 length little-endian) -- one node, host hashlib."""
+    import hashlib
+
+    return hashlib.sha256(bytes(root) + int(length).to_bytes(32, "little")).digest()
+
+
+def pairing_check(pairs, ctx=None) -> bool:
+    """KZG pairing_check (E/utils/bls.py; specs/deneb/polynomial-commitments.md:284,407,451):
+    prod e(P_i, Q_i) == 1 over compressed (48-byte G1, 96-byte G2) pairs; the identity is allowed,
+    an invalid encoding gives False."""
+    c = ctx or _native.context()
+    g1 = [bytes(p) for p, _ in pairs]
+    g2 = [bytes(q) for _, q in pairs]
+    if any(len(p) != 48 for p in g1) or any(len(q) != 96 for q in g2):
+        raise ValueError("need 48-byte G1 and 96-byte G2 encodings")
+    return c.check(c.lib.bls_pairing_check(c.h, b"".join(g1), b"".join(g2), len(g1))) == 1
+
+
+def g1_multi_exp(points48, scalars, ctx=None) -> bytes:
+    """KZG multi_exp / g1_lincomb: compressed sum [k_i] P_i; scalars are ints (0 <= k < 2^256)."""
+    c = ctx or _native.context()
+    pts = [bytes(p) for p in points48]
+    ks = [int(k) for k in scalars]
+    if len(pts) != len(ks):
+        raise ValueError("one scalar per point")
+    if any(len(p) != 48 for p in pts) or any(not 0 <= k < 1 << 256 for k in ks):
+        raise ValueError("need 48-byte points and 256-bit scalars")
+    out = ctypes.create_string_buffer(48)
+    rc = c.check(c.lib.bls_g1_multi_exp(c.h, b"".join(pts), b"".join(k.to_bytes(32, "big") for k in ks), len(pts),
+                                        out))
+    if rc != 1:
+        raise ValueError("invalid G1 point encoding")
+    return out.raw
+
+
 def fallback_stats(ctx=None) -> tuple[int, int]:
     """(batched final-exponentiation checks, bisection rounds) of the last batch call; (0, 0) if it passed."""
     c = ctx or _native.context()

@@ -25,6 +25,10 @@ enum Slot {
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
   S_AV_IO, S_AV_RSC, S_AV_PITEM, S_AV_SIG, S_AV_SOK, S_AV_H, S_AV_ST, S_AV_P, S_AV_Q, S_AV_F, S_AV_FT, S_AV_SEL,
   S_AV_FI, S_AV_RES, S_AV_U, S_AV_HCF, S_AV_FLAG,
+  // signing roots / merkleization
+  S_SZ_A, S_SZ_B, S_SZ_C, S_SZ_Z,
+  // KZG pieces
+  S_KZ_IN, S_KZ_P, S_KZ_Q, S_KZ_OK, S_KZ_OK2, S_KZ_F, S_KZ_FT, S_KZ_S, S_KZ_J, S_KZ_OUT,
   NSLOT
 };
 
@@ -1038,6 +1042,112 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
     ctx->j->bis_rounds = 1;
   }
   for (size_t b = 0; b < B; b++) out[b] = status[b] ? 1 : 0;
+  return 1;
+}
+
+int bls_signing_roots(bls_ctx* ctx, const uint8_t* object_roots32, const uint8_t* domains32, size_t domain_stride,
+                      size_t n, uint8_t* out32) {
+  API_ENTER(ctx);
+  if (n && (!object_roots32 || !domains32 || !out32)) return BLS_E_ARG;
+  if (domain_stride != 0 && domain_stride != 32) return BLS_E_ARG;
+  if (!n) return 1;
+  uint8_t *d_l, *d_r, *d_o;
+  const size_t nr = domain_stride ? n : 1;
+  SCR(S_SZ_A, 32 * n, d_l);
+  SCR(S_SZ_B, 32 * nr, d_r);
+  SCR(S_SZ_C, 32 * n, d_o);
+  CK(h2d(ctx, d_l, object_roots32, 32 * n));
+  CK(h2d(ctx, d_r, domains32, 32 * nr));
+  LK(launch_sha256_pairs(ctx->j->stream, d_l, d_r, domain_stride, n, d_o));
+  CK(d2h(ctx, out32, d_o, 32 * n));
+  return 1;
+}
+
+int bls_merkleize(bls_ctx* ctx, const uint8_t* chunks32, size_t n, int depth, uint8_t* root32) {
+  API_ENTER(ctx);
+  if ((n && !chunks32) || !root32 || depth < 0 || depth > 63) return BLS_E_ARG;
+  if (n > (1ull << depth)) return BLS_E_ARG;
+  uint8_t *d_a, *d_b, *d_z, *root;
+  SCR(S_SZ_A, 32 * (n ? n : 1), d_a);
+  SCR(S_SZ_B, 32 * ((n + 1) / 2 + 1), d_b);
+  SCR(S_SZ_Z, 32, d_z);
+  HIPCK(hipMemsetAsync(d_z, 0, 32, ctx->j->stream));
+  if (n == 0) {  // root of an all-zero tree: the zero hash of this depth
+    for (int l = 0; l < depth; l++) {
+      uint8_t* r;
+      LK(launch_merkleize(ctx->j->stream, d_z, d_a, 1, 1, d_z, &r));
+      HIPCK(hipMemcpyAsync(d_z, r, 32, hipMemcpyDeviceToDevice, ctx->j->stream));
+    }
+    CK(d2h(ctx, root32, d_z, 32));
+    return 1;
+  }
+  CK(h2d(ctx, d_a, chunks32, 32 * n));
+  LK(launch_merkleize(ctx->j->stream, d_a, d_b, n, depth, d_z, &root));
+  CK(d2h(ctx, root32, root, 32));
+  return 1;
+}
+
+int bls_pairing_check(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n) {
+  API_ENTER(ctx);
+  if (n && (!g1s48 || !g2s96)) return BLS_E_ARG;
+  if (n == 0) return 1;  // empty product
+  hipStream_t st = ctx->j->stream;
+  uint8_t* d_in;
+  G1A* P;
+  G2A* Q;
+  int *ok1, *ok2;
+  Fp12 *f, *ft, *fo;
+  SCR(S_KZ_IN, 144 * n, d_in);
+  SCR(S_KZ_P, n, P);
+  SCR(S_KZ_Q, n, Q);
+  SCR(S_KZ_OK, n, ok1);
+  SCR(S_KZ_OK2, n, ok2);
+  SCR(S_KZ_F, n, f);
+  SCR(S_KZ_FT, n / 8 + 16, ft);
+  SCR(S_FPART, 1, fo);
+  CK(h2d(ctx, d_in, g1s48, 48 * n));
+  CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
+  LK(launch_g1_decode_checked(st, d_in, n, P, ok1));
+  LK(launch_sig_validate(st, d_in + 48 * n, n, Q, ok2));
+  std::vector<int> a(n), b(n);
+  CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
+  CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
+  for (size_t i = 0; i < n; i++)
+    if (!a[i] || !b[i]) return 0;
+  LK(launch_miller_wave(st, P, Q, nullptr, n, f));  // identity pairs are skipped (value 1)
+  LK(launch_fp12_prod_vm(st, f, n, ft, fo));
+  return run_final_check(ctx, fo);
+}
+
+int bls_g1_multi_exp(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* scalars32, size_t n, uint8_t* out48) {
+  API_ENTER(ctx);
+  if ((n && (!g1s48 || !scalars32)) || !out48) return BLS_E_ARG;
+  hipStream_t st = ctx->j->stream;
+  uint8_t *d_in, *d_out;
+  G1A *P, *S;
+  int *ok, *live;
+  G1J *tmp, *sum;
+  SCR(S_KZ_IN, 80 * n, d_in);
+  SCR(S_KZ_P, n, P);
+  SCR(S_KZ_S, n, S);
+  SCR(S_KZ_OK, n, ok);
+  SCR(S_KZ_OK2, n, live);
+  SCR(S_KZ_J, 1024, tmp);
+  SCR(S_G1J, 1, sum);
+  SCR(S_KZ_OUT, 48, d_out);
+  if (n) {
+    CK(h2d(ctx, d_in, g1s48, 48 * n));
+    CK(h2d(ctx, d_in + 48 * n, scalars32, 32 * n));
+    LK(launch_g1_decode_checked(st, d_in, n, P, ok));
+    std::vector<int> a(n);
+    CK(d2h(ctx, a.data(), ok, n * sizeof(int)));
+    for (size_t i = 0; i < n; i++)
+      if (!a[i]) return 0;
+    LK(launch_g1_scale(st, P, d_in + 48 * n, n, S, live));
+  }
+  LK(launch_g1_sum_aff(st, S, live, n, tmp, sum));
+  LK(launch_g1_compress(st, sum, d_out, nullptr));
+  CK(d2h(ctx, out48, d_out, 48));
   return 1;
 }
 

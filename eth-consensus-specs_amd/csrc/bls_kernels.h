@@ -21,6 +21,13 @@ hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const i
 hipError_t launch_av_pairs(hipStream_t st, size_t total, const uint32_t* pair_item, const int* status, const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2);
 // out[b] = product of in[io[b] + b .. io[b + 1] + b] (the AggregateVerify batch's per-item segments)
 hipError_t launch_fp12_seg_prod(hipStream_t st, const Fp12* in, const uint64_t* io, size_t B, Fp12* out);
+// SHA-256 of 64-byte nodes (bls_ssz.hip): signing roots and SSZ merkleization
+hipError_t launch_sha256_pairs(hipStream_t st, const uint8_t* left, const uint8_t* right, size_t rstride, size_t n,
+                               uint8_t* out);
+hipError_t launch_merkleize(hipStream_t st, uint8_t* a, uint8_t* b, size_t n, int depth, uint8_t* zero, uint8_t** root);
+// KZG: checked G1 decode (identity allowed), per-point scalar products for multi_exp
+hipError_t launch_g1_decode_checked(hipStream_t st, const uint8_t* in48, size_t n, G1A* out, int* ok);
+hipError_t launch_g1_scale(hipStream_t st, const G1A* P, const uint8_t* k32, size_t n, G1A* out, int* live);
 hipError_t launch_verdicts(hipStream_t st, const int* status, const uint8_t* bad, size_t B, uint8_t* out);
 hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint8_t* out);
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out);

@@ -329,6 +329,41 @@ __global__ void __launch_bounds__(64) k_av_pairs(size_t total, const uint32_t* p
   Q2[t + b] = H[t];
 }
 
+// (6) KZG pieces: checked G1 decoding that accepts the
+//     identity (validate_kzg_g1, specs/deneb/polynomial-commitments.md), and the
+//     per-point products [k_i] P_i of multi_exp (summed by k_g1_sum_aff).
+__global__ void __launch_bounds__(64) k_g1_decode_checked(const uint8_t* in48, size_t n, G1A* out, int* ok) {
+  const size_t i = gtid();
+  if (i >= n) return;
+  G1A a{fp_zero(), fp_zero(), true};
+  const int d = g1_decompress(a, in48 + 48 * i);
+  int v = 0;
+  if (d == DEC_INFINITY) {
+    a = G1A{fp_zero(), fp_zero(), true};
+    v = 1;
+  } else if (d == DEC_OK) {
+    v = g1_in_subgroup(jac_from_aff(a)) ? 1 : 0;
+  }
+  if (!v) a = G1A{fp_zero(), fp_zero(), true};
+  out[i] = a;
+  ok[i] = v;
+}
+
+// scalars: 32-byte big-endian integers; out[i] = [k_i] P_i (affine), live[i] = 0 for the identity
+__global__ void __launch_bounds__(64) k_g1_scale(const G1A* P, const uint8_t* k32, size_t n, G1A* out, int* live) {
+  const size_t i = gtid();
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int w = 0; w < 8; w++) {
+    const uint8_t* b = k32 + 32 * i + 28 - 4 * w;
+    k[w] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+  }
+  G1A r{fp_zero(), fp_zero(), true};
+  if (!P[i].inf) r = jac_to_aff(jac_mul_u256(jac_from_aff(P[i]), k));
+  out[i] = r;
+  live[i] = r.inf ? 0 : 1;
+}
+
 // Verdicts: valid iff the per-item checks passed and bisection did not isolate it.
 __global__ void k_verdicts(const int* status, const uint8_t* bad, size_t B, uint8_t* out) {
   size_t i = gtid();
@@ -503,6 +538,16 @@ hipError_t launch_av_pairs(hipStream_t st, size_t total, const uint32_t* pair_it
                            const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2) {
   if (!total) return hipSuccess;
   LAUNCH(k_av_pairs, nblk(total, 64), 64, st, total, pair_item, status, rsc, pk, H, P2, Q2);
+  return hipSuccess;
+}
+hipError_t launch_g1_decode_checked(hipStream_t st, const uint8_t* in48, size_t n, G1A* out, int* ok) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_g1_decode_checked, nblk(n, 64), 64, st, in48, n, out, ok);
+  return hipSuccess;
+}
+hipError_t launch_g1_scale(hipStream_t st, const G1A* P, const uint8_t* k32, size_t n, G1A* out, int* live) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_g1_scale, nblk(n, 64), 64, st, P, k32, n, out, live);
   return hipSuccess;
 }
 hipError_t launch_verdicts(hipStream_t st, const int* status, const uint8_t* bad, size_t B, uint8_t* out) {

@@ -125,6 +125,32 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
  * specs/electra/beacon-chain.md:1577-1588.  Returns 1 or BLS_E_*. */
 int bls_registry_append(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid);
 
+/* ---- signing roots and SSZ merkleization ------ */
+/* out32[i] = SHA-256(object_roots32[32 i ..] || domains32[domain_stride i ..]):
+ * compute_signing_root  <- specs/phase0/beacon-chain.md:953-962 (SigningData
+ * :317-320).  domain_stride 0 = one domain for all, 32 = one per item.
+ * Returns 1 or BLS_E_*. */
+int bls_signing_roots(bls_ctx* ctx, const uint8_t* object_roots32, const uint8_t* domains32, size_t domain_stride,
+                      size_t n, uint8_t* out32);
+/* SSZ merkleize(chunks, limit): n 32-byte chunks, tree of 2^depth leaves
+ * (depth >= ceil(log2 n); missing leaves are zero chunks).  n = 0 gives the
+ * zero-subtree root of that depth.  Returns 1 or BLS_E_*. */
+int bls_merkleize(bls_ctx* ctx, const uint8_t* chunks32, size_t n, int depth, uint8_t* root32);
+
+/* ---- KZG pieces ---------------------------------- */
+/* pairing_check  <- E/utils/bls.py pairing_check (used by
+ * specs/deneb/polynomial-commitments.md:284,407,451): 1 iff
+ * prod_i e(P_i, Q_i) == 1 for compressed P_i (48 B, identity allowed) and
+ * Q_i (96 B, identity allowed); both subgroup-checked.  0 if the product is
+ * not 1 or any encoding is invalid.  Returns 1 / 0 / BLS_E_*. */
+int bls_pairing_check(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n);
+/* multi_exp / g1_lincomb  <- E/utils/bls.py multi_exp
+ * (specs/deneb/polynomial-commitments.md g1_lincomb): out48 = compressed
+ * sum_i [k_i] P_i, scalars as 32-byte big-endian integers.  1 on success, 0
+ * if a point encoding is invalid (the reference raises).  Returns 1 / 0 /
+ * BLS_E_*. */
+int bls_g1_multi_exp(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* scalars32, size_t n, uint8_t* out48);
+
 /* Fallback statistics of the last batch call on this context: the number of
  * batched final-exponentiation checks and bisection rounds it ran (both 0
  * when the whole-batch check passed).  Returns 0 or BLS_E_*. */

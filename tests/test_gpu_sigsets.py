@@ -164,3 +164,87 @@ def test_signature_sets_block(b):
             shim.FastAggregateVerify([pks[k] for k in committees[1]], m[1], fav_sigs[0])
     # outside the block the shim verifies immediately again
     assert shim.FastAggregateVerify([pks[k] for k in committees[1]], m[1], fav_sigs[0]) is False
+
+
+def test_signing_roots_and_merkleize(b):
+    """GPU SHA-256 node hashing against hashlib (compute_signing_root, SSZ merkleize with zero padding)."""
+    import hashlib
+    import os
+
+    rng = np.random.default_rng(11)
+    roots = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(300)]
+    dom = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    assert b.compute_signing_roots(roots, dom) == [hashlib.sha256(r + dom).digest() for r in roots]
+    doms = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(300)]
+    assert b.compute_signing_roots(roots, doms) == [hashlib.sha256(r + d).digest() for r, d in zip(roots, doms)]
+    assert b.compute_signing_roots([], dom) == []
+
+    def ref_merkleize(chunks, limit=None):
+        size = len(chunks) if limit is None else limit
+        depth = max(size - 1, 0).bit_length()
+        layer = list(chunks) or [bytes(32)]
+        zero = bytes(32)
+        if not chunks:
+            for _ in range(depth):
+                zero = hashlib.sha256(zero + zero).digest()
+            return zero
+        for _ in range(depth):
+            if len(layer) % 2:
+                layer.append(zero)
+            layer = [hashlib.sha256(layer[i] + layer[i + 1]).digest() for i in range(0, len(layer), 2)]
+            zero = hashlib.sha256(zero + zero).digest()
+        return layer[0]
+
+    for n, limit in [(1, None), (2, None), (5, None), (5, 8), (7, 1024), (300, None), (0, 16), (1, 1), (3, 2 ** 20)]:
+        ch = roots[:n]
+        assert b.merkleize(ch, limit) == ref_merkleize(ch, limit), (n, limit)
+    # the altair/bls signing root pin: SigningData(object_root, domain) of the deposit-cli known answer shape
+    obj = os.urandom(32)
+    assert b.compute_signing_roots([obj], dom)[0] == ref_merkleize([obj, dom])
+
+
+def _golden(name):
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)) as fh:
+        return json.load(fh)
+
+
+def _neg_g1(p48):
+    return p48 if p48[0] & 0x40 else bytes([p48[0] ^ 0x20]) + p48[1:]
+
+
+def test_kzg_pairing_check_trusted_setup(b):
+    """e([tau^i] G1, [tau^j] G2) = e([tau^(i+j)] G1, G2) on the KZG trusted setup."""
+    ts = _golden("trusted_setup.json")
+    g1 = [bytes.fromhex(x[2:]) for x in ts["g1_monomial"][:8]]
+    g2 = [bytes.fromhex(x[2:]) for x in ts["g2_monomial"][:4]]
+    for i, j in [(1, 1), (2, 3), (0, 2), (3, 1)]:
+        assert b.pairing_check([(g1[i], g2[j]), (_neg_g1(g1[i + j]), g2[0])]) is True
+        assert b.pairing_check([(g1[i], g2[j]), (_neg_g1(g1[i + j + 1]), g2[0])]) is False
+    assert b.pairing_check([]) is True
+    assert b.pairing_check([(G1_INF, g2[1]), (g1[1], G2_INF)]) is True   # identities contribute 1
+    assert b.pairing_check([(g1[1], g2[1])]) is False
+    assert b.pairing_check([(b"\x40" + bytes(47), g2[1])]) is False       # invalid encoding
+
+
+def test_kzg_g1_multi_exp(b):
+    ts = _golden("trusted_setup.json")
+    lag = [bytes.fromhex(x[2:]) for x in ts["g1_lagrange"][:64]]
+    gen = bytes.fromhex(ts["g1_monomial"][0][2:])
+    # sum of all 4096 Lagrange points with unit scalars is the generator
+    lag_all = [bytes.fromhex(x[2:]) for x in ts["g1_lagrange"]]
+    assert b.g1_multi_exp(lag_all, [1] * len(lag_all)) == gen
+    ks = [3, 5, 7, O.R - 1, 2 ** 255 + 12345]
+    assert b.g1_multi_exp([gen] * 5, ks) == OC.SkToPk(sum(ks) % O.R)
+    rng = np.random.default_rng(3)
+    k = [int.from_bytes(bytes(rng.integers(0, 256, 32, dtype=np.uint8)), "big") % O.R for _ in range(64)]
+    # linearity: split the scalars, add the two results with the per-call AggregatePKs-free path
+    whole = b.g1_multi_exp(lag, k)
+    again = b.g1_multi_exp(lag + lag, [x // 2 for x in k] + [x - x // 2 for x in k])
+    assert whole == again
+    assert b.g1_multi_exp([], []) == G1_INF
+    assert b.g1_multi_exp([gen], [O.R]) == G1_INF
+    with pytest.raises(ValueError):
+        b.g1_multi_exp([b"\x40" + bytes(47)], [1])
