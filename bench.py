@@ -256,8 +256,16 @@ def main():
         units = B + (1 if dom == "miller" else 0)
         ops = fme[dom] * FME_OPS * units + (19 * SHA_OPS * B if dom == "fav_hash" else 0)
         ach = ops / avg_s / 1e12
+        traffic, tsrc = None, None
+        try:  # HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE pass (a PMC run cannot be live)
+            with open(os.path.join(ROOT, "tools", "pmc_traffic.json")) as fh:
+                tj = json.load(fh)
+            traffic, tsrc = tj["bytes_per_dispatch"].get(dom), tj["source"]
+        except (OSError, ValueError, KeyError):
+            pass
         roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4), "peak": round(PEAK_INT_OPS / 1e12, 2),
-                "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5), "traffic": None,
+                "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5), "traffic": traffic,
+                "traffic_source": tsrc,
                 "ops_per_launch": ops, "avg_launch_ms": round(avg_s * 1e3, 4)}
     if roof is not None:
         roof["frac_of_measured_mad_rate"] = round(roof["achieved"] * 1e12 / MEASURED_MAD_OPS, 5)
