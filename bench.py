@@ -29,8 +29,8 @@ import time
 import numpy as np
 
 # before torch / HIP start (multi-GPU ranks initialise HIP through torch first): see _native.hw_queue_policy
-if not os.environ.get("BLSMI355X_KEEP_HW_QUEUES") and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+if not os.environ.get("BLSMI355X_KEEP_HW_QUEUES") and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 20:
+    os.environ["GPU_MAX_HW_QUEUES"] = "20"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "eth-consensus-specs_amd")):
@@ -42,8 +42,8 @@ PEAK_INT_OPS = 256 * 4 * 32 / 2 * 2.4e9  # v_mad_u64_u32 is half rate on gfx950:
 FME_OPS = 288  # one 381-bit Montgomery multiplication = 288 v_mad_u64_u32
 SHA_OPS = 2400  # one SHA-256 compression
 MEASURED_MAD_OPS = 31.3e12  # sustained v_mad_u64_u32 lane-ops/s, profiles/r01_s2_madrate_microbench.txt
-SINGLE_KERNEL = ("miller", "fav_gather")
-LANE_KERNELS = ("miller", "sig_vm")  # one lane per item, full register file (bls_miller_lane.hip, bls_chain_lane.hip)
+SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
+LANE_KERNELS = ("miller", "miller_lines", "sig_vm")  # one lane per item, full register file (bls_miller_lane.hip, bls_chain_lane.hip)
 GATHER_BYTES_PER_KEY = 4 + 96 + 1  # u32 index + affine (x, y) + validity byte
 
 
@@ -54,7 +54,11 @@ def model_fme(n: int):
         "sig_decode": 1200,             # signature decompression (Fp2 square root)
         "sig_vm": 1200 + 1000 + 400,    # G2 subgroup check, RLC G1, RLC G2 (MSM share)
         "fav_hash": 6600,
-        "miller": 4400,
+        # Miller loop, 4400 FME per pair, split between its two kernels in proportion to the products each
+        # executes: k_miller_acc (f: 62 Fp12 squarings x 36 + 68 sparse line products x 43 = 5156) and
+        # k_miller_lines (T: 63 doublings x 26 + 5 additions x 35 = 1813)
+        "miller": 4400 * 5156 / 6969,
+        "miller_lines": 4400 * 1813 / 6969,
     }
 
 
@@ -253,8 +257,8 @@ def main():
         # rocprofv3 summary's average for that kernel can be set beside this hipEvent figure
         dom = max((k for k in SINGLE_KERNEL if k in kern and kern[k][1]), key=lambda k: kern[k][0])
         avg_s = kern[dom][0] / kern[dom][1] * 1e-3
-        units = B + (1 if dom == "miller" else 0)
-        ops = fme[dom] * FME_OPS * units + (19 * SHA_OPS * B if dom == "fav_hash" else 0)
+        units = B
+        ops = round(fme[dom] * FME_OPS * units) + (19 * SHA_OPS * B if dom == "fav_hash" else 0)
         ach = ops / avg_s / 1e12
         traffic, tsrc = None, None
         try:  # HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE pass (a PMC run cannot be live)

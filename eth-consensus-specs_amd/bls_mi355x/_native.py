@@ -10,13 +10,13 @@ import ctypes
 import os
 import threading
 
-HW_QUEUES = 16
+HW_QUEUES = 20  # 5 FAV jobs x 3 streams + the default/copy streams
 
 
 def hw_queue_policy() -> None:
     """The library keeps up to BLS_FAV_JOBS x 3 streams busy; with HIP's default of 4 hardware queues per
     process, streams share queues and a long one-lane-per-item kernel blocks every kernel queued behind it
-    (measured: 687k -> 838k FAV/s at 8+ queues).  Raise GPU_MAX_HW_QUEUES before the HIP runtime starts
+    (measured: 687k -> 838k FAV/s at 8+ queues; 5 jobs: 1.00M at 16, 1.02M at 20).  Raise GPU_MAX_HW_QUEUES before the HIP runtime starts
     (it reads the variable once), unless BLSMI355X_KEEP_HW_QUEUES is set.  The C library's load-time
     constructor applies the same policy for non-Python hosts."""
     if os.environ.get("BLSMI355X_KEEP_HW_QUEUES"):

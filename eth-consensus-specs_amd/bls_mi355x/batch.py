@@ -17,9 +17,11 @@ import numpy as np
 
 from . import _native
 
-FAV_JOBS = 4  # BLS_FAV_JOBS in include/blsmi355x.h: per-context job slots
+# per-context job slots with streams: BLS_FAV_JOBS_INIT (default 5; 6 hits HSA_STATUS_ERROR_OUT_OF_RESOURCES) of the
+# BLS_FAV_JOBS = 8 in include/blsmi355x.h, read by the library at bls_ctx_create
+FAV_JOBS = max(1, min(8, int(os.environ.get("BLS_FAV_JOBS_INIT", "5"))))
 # batches kept in flight by run_pipelined (<= FAV_JOBS)
-FAV_DEPTH = max(1, min(FAV_JOBS, int(os.environ.get("BLS_FAV_DEPTH", "4"))))
+FAV_DEPTH = max(1, min(FAV_JOBS, int(os.environ.get("BLS_FAV_DEPTH", str(FAV_JOBS)))))
 
 
 def _ptr(a: np.ndarray):

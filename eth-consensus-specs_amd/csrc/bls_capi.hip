@@ -19,7 +19,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ,
+  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
@@ -62,6 +62,7 @@ struct Job {
 
 struct bls_ctx {
   int device = 0;
+  int njobs = 5;  // job slots with streams: BLS_FAV_JOBS_INIT (default 5, at most BLS_FAV_JOBS)
   Job jobs[BLS_FAV_JOBS];
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
@@ -81,7 +82,7 @@ struct bls_ctx {
 
 static const char* const PROF_NAMES[] = {"fav_gather", "sig_decode", "fav_hash", "g2_sum",        "sig_pair", "miller",
                                          "fp12_prod",  "final_exp",  "fav_finish", "partials_prod", "sig_vm",
-                                         "msm"};
+                                         "msm",        "miller_lines"};
 static const int PROF_N = sizeof(PROF_NAMES) / sizeof(PROF_NAMES[0]);
 
 namespace {
@@ -245,7 +246,7 @@ struct JobScope {
 };
 #define JOB_ENTER(ctx, job)                                  \
   API_ENTER(ctx);                                            \
-  if ((job) < 0 || (job) >= BLS_FAV_JOBS) return BLS_E_ARG;  \
+  if ((job) < 0 || (job) >= ctx->njobs) return BLS_E_ARG;     \
   JobScope job_scope_(ctx, job)
 
 // Hardware-queue policy (see bls_mi355x/_native.py hw_queue_policy): the
@@ -256,7 +257,7 @@ struct JobScope {
 __attribute__((constructor)) static void bls_hw_queue_policy() {
   if (getenv("BLSMI355X_KEEP_HW_QUEUES")) return;
   const char* v = getenv("GPU_MAX_HW_QUEUES");
-  if (!v || atoi(v) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+  if (!v || atoi(v) < 20) setenv("GPU_MAX_HW_QUEUES", "20", 1);
 }
 
 extern "C" {
@@ -299,8 +300,11 @@ int bls_ctx_create(int device, bls_ctx** out) {
   c->device = device;
   int prio_lo = 0, prio_hi = 0;  // the MSM branch is latency-bound: schedule it first
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  for (Job& J : c->jobs) {
-    if (!job_init(J, prio_hi)) {
+  // All job streams are created here, before any kernel runs (streams created
+  // later, between launches, were measured to hit HSA_STATUS_ERROR_OUT_OF_RESOURCES).
+  if (const char* v = getenv("BLS_FAV_JOBS_INIT")) c->njobs = atoi(v) < 1 ? 1 : atoi(v) > BLS_FAV_JOBS ? BLS_FAV_JOBS : atoi(v);
+  for (int k = 0; k < c->njobs; ++k) {
+    if (!job_init(c->jobs[k], prio_hi)) {
       bls_ctx_destroy(c);
       return BLS_E_DEVICE;
     }
@@ -721,6 +725,14 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_MSMF, msm_scratch_fd(), msmf);
   SCR(S_HCF, h2c_scratch_fd(B), hcf);
   SCR(S_RPJ, B, rpj);
+  // Miller loop of (r_i apk_i, H_i): split (G2 lines on stream2 right after
+  // hash_to_G2, f accumulation on stream1) unless BLS_ML_MODE=fused / st1
+  static const int ml_mode = [] {
+    const char* m = getenv("BLS_ML_MODE");
+    return !m ? 2 : !strcmp(m, "fused") ? 0 : !strcmp(m, "st1") ? 1 : 2;
+  }();
+  uint32_t* mlines = nullptr;
+  if (ml_mode) SCR(S_MLINES, miller_lines_u32(B), mlines);
   SCR(S_SAFF, 1, saff);
   SCR(S_MSTAT, B, dstat);
   SCR(S_F, B + 2, f);
@@ -740,6 +752,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   HIPCK(hipStreamWaitEvent(st2, ctx->j->ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, hcf, H, flag));
+  if (ml_mode == 2) PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
   HIPCK(hipEventRecord(ctx->j->ev_join, st2));
   PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
   HIPCK(hipEventRecord(ctx->j->ev_sig, st3));
@@ -766,7 +779,11 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     PROF(5, launch_miller2(st, rP, H, status, B, f));
     PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
   } else {
-    PROF(5, launch_miller_lane(st, rP, H, status, B, f));
+    if (ml_mode == 1) PROF(12, launch_miller_lines(st, H, B, mlines));
+    if (ml_mode)
+      PROF(5, launch_miller_acc(st, rP, H, status, B, mlines, f));
+    else
+      PROF(5, launch_miller_lane(st, rP, H, status, B, f));
     PROF(6, launch_fp12_prod_vm(st, f, B, ft, f + B));
   }
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_msm, 0));

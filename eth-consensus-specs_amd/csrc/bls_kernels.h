@@ -56,6 +56,12 @@ size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
 // one lane per pair (bls_miller_lane.hip): f[i] = Miller value of pair i (1 if skipped)
 hipError_t launch_miller_lane(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
+// the same Miller values in two kernels (G2 lines, then f); L: miller_lines_u32(n) words of scratch
+constexpr int MILLER_NLINES = 68;  // 63 doublings + 5 additions (|x| = 0xd201000000010000)
+size_t miller_lines_u32(size_t n);
+hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L);
+hipError_t launch_miller_acc(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                             Fp12* f);
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
 // nsel independent checks: out[b] = (FE(f[sel[b]]) == 1)

@@ -37,8 +37,8 @@ extern "C" {
 
 typedef struct bls_ctx bls_ctx;
 
-/* FAV batches that may be in flight together on one context (bls_fav_job_*). */
-#define BLS_FAV_JOBS 4
+/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 5) get streams. */
+#define BLS_FAV_JOBS 8
 
 /* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
 int bls_ctx_create(int device, bls_ctx** out);

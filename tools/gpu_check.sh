@@ -16,7 +16,7 @@ for s in $STEPS; do
         > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
       tail -3 "$OUT/pytest.log" ;;
     bench)
-      timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 > "$OUT/bench.json" 2> "$OUT/bench.err" \
+      timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
         || { tail -30 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
     benchq)
