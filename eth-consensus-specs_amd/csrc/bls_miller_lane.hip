@@ -150,9 +150,13 @@ __global__ void __launch_bounds__(64) k_miller_acc(const G1A* P, const G2A* Q, c
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = f12sqr(f);
+    // keep the line loads after the squaring: hoisted above it they hold 72
+    // registers through the squaring's Fp6 temporaries and push f to scratch
+    asm volatile("" ::: "memory");
     f = f12line(f, ml_load(Li, n, 0), f2mulfp(ml_load(Li, n, 24), nxP), f2mulfp(ml_load(Li, n, 48), yP));
     Li += step;
     if ((X_ABS >> b) & 1ull) {
+      asm volatile("" ::: "memory");
       f = f12line(f, ml_load(Li, n, 0), f2mulfp(ml_load(Li, n, 24), nxP), f2mulfp(ml_load(Li, n, 48), yP));
       Li += step;
     }
