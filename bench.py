@@ -12,8 +12,15 @@ random-linear-combination Miller loops, one shared final exponentiation
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
 --gpus N): weak scaling, each rank owns its own batch; the ranks' 576-byte
-Fp12 Miller partials are all-gathered over RCCL (torch.distributed "nccl")
-and every rank final-exponentiates the product.
+Fp12 Miller partials are all-gathered by the library over RCCL
+(bls_fav_job_check_comm: ncclAllGather on the device, xGMI) and every rank
+final-exponentiates the product.  torch.distributed (gloo) is only the
+control plane: rendezvous, the RCCL unique id, barriers, max over ranks.
+
+Roofline: after the timed region, a few passes run one batch at a time with
+per-kernel hipEvent timing (bls_profile_*), so each kernel's average is its
+own execution time (with five batches in flight a hipEvent pair also spans
+the wait for the queue and CUs); `roofline` uses those averages.
 
 Prints ONE JSON line on rank 0.
 """
@@ -44,7 +51,10 @@ SHA_OPS = 2400  # one SHA-256 compression
 MEASURED_MAD_OPS = 31.3e12  # sustained v_mad_u64_u32 lane-ops/s, profiles/r01_s2_madrate_microbench.txt
 SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
 LANE_KERNELS = ("miller", "miller_lines", "sig_vm")  # one lane per item, full register file (bls_miller_lane.hip, bls_chain_lane.hip)
-GATHER_BYTES_PER_KEY = 4 + 96 + 1  # u32 index + affine (x, y) + validity byte
+GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
+# profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
+KERNEL_SYMBOL = {"miller": "k_miller_acc", "miller_lines": "k_miller_lines", "fav_gather": "k_fav_gather<16>"}
+ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 
 
 def model_fme(n: int):
@@ -150,6 +160,38 @@ def cpu_baseline(n: int, seconds: float, cores: int, reg_n: int = 1 << 14, per_c
                       f"{res[0][1]:.1f} s"}
 
 
+def percall_latency(reps: int = 15):
+    """Median wall-clock latency of the drop-in per-call API (E/utils/bls.py:141-177 call pattern: one ctypes
+    call per verification, host buffers): Verify and FastAggregateVerify(n = 512), beside the C port's per-call
+    time on one host core for the same inputs."""
+    import statistics
+
+    from bls_mi355x.backend import mi355x_bls as M
+    from oracle import bls_oracle_c as OC
+
+    sks = list(range(1001, 1001 + 512))
+    pks = [OC.SkToPk(k) for k in sks]
+    m = hashlib.sha256(b"percall").digest()
+    sig1 = OC.Sign(sks[0], m)
+    sig512 = OC.Sign(sum(sks), m)
+
+    def med(fn, r):
+        ts = []
+        for _ in range(r):
+            t = time.perf_counter()
+            assert fn()
+            ts.append(time.perf_counter() - t)
+        return round(statistics.median(ts) * 1e3, 3)
+
+    M.Verify(pks[0], m, sig1)  # warm (first-call scratch allocation)
+    M.FastAggregateVerify(pks, m, sig512)
+    return {"verify_ms": med(lambda: M.Verify(pks[0], m, sig1), reps),
+            "fav512_ms": med(lambda: M.FastAggregateVerify(pks, m, sig512), reps),
+            "cpu_port_verify_ms": med(lambda: OC.Verify(pks[0], m, sig1), 3),
+            "cpu_port_fav512_ms": med(lambda: OC.FastAggregateVerify(pks, m, sig512), 3),
+            "note": "median wall-clock per call incl. ctypes + H2D/D2H; CPU port = oracle/bls_oracle.c on 1 core"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,6 +206,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight (no overlap of passes)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel hipEvent timing")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batch call")
+    ap.add_argument("--roofline-passes", type=int, default=5, help="one-batch-at-a-time passes timed per kernel")
+    ap.add_argument("--no-percall", action="store_true", help="skip the drop-in per-call latency figures")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -172,25 +216,28 @@ def main():
     os.environ["BLSMI355X_DEVICE"] = str(local)
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")  # control plane only; the partials travel over RCCL inside the library
 
     from bls_mi355x import _native, batch
 
     ctx = _native.context()
     dev_name, cus = ctx.device_info()
+    if dist is not None:
+        from bls_mi355x import dist as bdist
+        from torch.distributed import distributed_c10d as c10d
+
+        bdist.init_comm(ctx, rank, world, c10d._get_default_store())
 
     def barrier_sync():
         ctx.check(ctx.lib.bls_sync(ctx.h))
         if dist is not None:
             import torch
 
-            torch.cuda.synchronize()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
             dist.barrier()
-            torch.cuda.synchronize()
 
     # ---- setup (untimed) ----------------------------------------------------
     t_setup = time.perf_counter()
@@ -201,49 +248,39 @@ def main():
     rb = batch.ResidentFavBatch(idx, offs, msgs, sigs, ctx=ctx)
     setup_s = time.perf_counter() - t_setup
 
-    from bls_mi355x.dist import allgather_partials
-
-    exchange = (lambda p: allgather_partials(p, device=f"cuda:{local}")) if dist is not None else None
-
-    def passes(k: int) -> list:
-        """k passes over the batch; by default pass j+1 is submitted before pass j is final-exponentiated
-        (two batches in flight, bls_fav_job_*), so every pass completes inside the call."""
+    def passes(k: int, depth: int | None = None) -> list:
+        """k passes over the batch; by default pass j+1.. are submitted before pass j is final-exponentiated
+        (up to FAV_DEPTH batches in flight, bls_fav_job_*), so every pass completes inside the call."""
         if args.no_pipeline:
-            return [step(os.urandom(32)) for _ in range(k)]
-        return rb.run_pipelined([os.urandom(32) for _ in range(k)], exchange)
-
-    def step(seed32: bytes) -> bool:
-        part = rb.partial(seed32)
-        if dist is not None:
-            part = allgather_partials(part, device=f"cuda:{local}")
-        ok = rb.check_partials(part)
-        rb.finish(ok)
-        return ok
+            depth = 1
+        d = batch.FAV_DEPTH if depth is None else depth
+        return rb.run_pipelined([os.urandom(32) for _ in range(k)], depth=d, comm=dist is not None)
 
     if args.warmup:
         assert all(passes(args.warmup)), "warmup batch failed the pairing check"
     v = rb.verdicts()
     assert v.all(), f"{(~v).sum()} valid aggregates rejected"
 
-    prof = batch.Profiler(ctx)
-    if not args.no_profile:
-        prof.start()
     barrier_sync()
     t0 = time.perf_counter()
     oks = passes(args.steps)
     barrier_sync()
     dt = time.perf_counter() - t0
-    kern = prof.read() if not args.no_profile else {}
-    if not args.no_profile:
-        prof.stop()
     assert all(oks)
     if dist is not None:
         import torch
 
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-
+    # per-kernel execution times: one batch at a time, hipEvents around each launch (after the timed region)
+    kern = {}
+    if not args.no_profile and args.roofline_passes > 0:
+        prof = batch.Profiler(ctx)
+        prof.start()
+        assert all(passes(args.roofline_passes, depth=1))
+        kern = prof.read()
+        prof.stop()
     B, n = args.batch, args.committee
     ms_step = dt / args.steps * 1e3
     value = B * world * args.steps / dt
@@ -267,10 +304,21 @@ def main():
             traffic, tsrc = tj["bytes_per_dispatch"].get(dom), tj["source"]
         except (OSError, ValueError, KeyError):
             pass
-        roof = {"bound": "valu-int", "kernel": dom, "achieved": round(ach, 4), "peak": round(PEAK_INT_OPS / 1e12, 2),
-                "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5), "traffic": traffic,
-                "traffic_source": tsrc,
-                "ops_per_launch": ops, "avg_launch_ms": round(avg_s * 1e3, 4)}
+        roof = {"bound": "valu-int", "kernel": dom, "symbol": KERNEL_SYMBOL.get(dom), "achieved": round(ach, 4),
+                "peak": round(PEAK_INT_OPS / 1e12, 2), "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5),
+                "traffic": traffic, "traffic_source": tsrc, "ops_per_launch": ops,
+                "avg_launch_ms": round(avg_s * 1e3, 4),
+                "avg_source": f"hipEvents around each launch, {args.roofline_passes} one-batch-at-a-time passes"}
+        try:  # the committed rocprofv3 --kernel-trace --stats average of the same kernel (same build)
+            with open(ROCPROF_AVG) as fh:
+                rj = json.load(fh)
+            r_ms = rj["avg_ms"].get(KERNEL_SYMBOL.get(dom))
+            if r_ms:
+                roof["rocprof_avg_ms"] = r_ms
+                roof["rocprof_source"] = rj["source"]
+                roof["frac_rocprof"] = round(ops / (r_ms * 1e-3) / PEAK_INT_OPS, 5)
+        except (OSError, ValueError, KeyError):
+            pass
     if roof is not None:
         roof["frac_of_measured_mad_rate"] = round(roof["achieved"] * 1e12 / MEASURED_MAD_OPS, 5)
         if dom in LANE_KERNELS:  # one lane per item: the launch occupies ceil(B/64) of the 1024 SIMDs
@@ -291,6 +339,9 @@ def main():
         v2 = batch.fast_aggregate_verify_batch(idx, offs, msgs, sigs, ctx=ctx)
         e2e = round(B / (time.perf_counter() - t1), 1)
         assert v2.all()
+    percall = None
+    if rank == 0 and world == 1 and not args.no_percall:
+        percall = percall_latency()
     total_fme = 11 * n + 14789
     pipeline_ops = (total_fme * FME_OPS + 19 * SHA_OPS) * B * world * args.steps + 9268 * FME_OPS * args.steps
     pipeline_frac = pipeline_ops / dt / (PEAK_INT_OPS * world)
@@ -308,6 +359,7 @@ def main():
         "kernels_avg_ms": kernels_ms,
         "gather_hbm_gbs": gather_gbs,
         "host_buffers_fav_s": e2e,
+        "percall": percall,
         "device": dev_name, "cus": cus, "setup_s": round(setup_s, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -319,6 +371,7 @@ def main():
         print(json.dumps(out), flush=True)
     rb.free()
     if dist is not None:
+        bdist.destroy_comm(ctx)
         dist.destroy_process_group()
 
 

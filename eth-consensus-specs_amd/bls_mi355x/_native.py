@@ -14,19 +14,15 @@ HW_QUEUES = 20  # 5 FAV jobs x 3 streams + the default/copy streams
 
 
 def hw_queue_policy() -> None:
-    """The library keeps up to BLS_FAV_JOBS x 3 streams busy; with HIP's default of 4 hardware queues per
+    """The library keeps up to BLS_FAV_JOBS_INIT x 3 streams busy; with HIP's default of 4 hardware queues per
     process, streams share queues and a long one-lane-per-item kernel blocks every kernel queued behind it
-    (measured: 687k -> 838k FAV/s at 8+ queues; 5 jobs: 1.00M at 16, 1.02M at 20).  Raise GPU_MAX_HW_QUEUES before the HIP runtime starts
-    (it reads the variable once), unless BLSMI355X_KEEP_HW_QUEUES is set.  The C library's load-time
-    constructor applies the same policy for non-Python hosts."""
-    if os.environ.get("BLSMI355X_KEEP_HW_QUEUES"):
+    (measured: 687k -> 838k FAV/s at 8+ queues; 5 jobs: 1.00M at 16, 1.02M at 20).  HIP reads
+    GPU_MAX_HW_QUEUES once, when it starts, so this sets it at import -- only when the variable is unset (an
+    explicit setting is kept) and unless BLSMI355X_KEEP_HW_QUEUES is set.  The C library itself never changes
+    the process environment (other hosts set the variable themselves)."""
+    if os.environ.get("BLSMI355X_KEEP_HW_QUEUES") or "GPU_MAX_HW_QUEUES" in os.environ:
         return
-    try:
-        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-    except ValueError:
-        cur = 0
-    if cur < HW_QUEUES:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 
 hw_queue_policy()
@@ -95,6 +91,19 @@ _SIGS = {
     "bls_profile_enable": (_ip, [_vp, _ip]),
     "bls_profile_read": (_ip, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), _ip]),
     "bls_profile_name": (ctypes.c_char_p, [_ip]),
+    "bls_registry_generation": (ctypes.c_uint64, [_vp]),
+    "bls_point_decode": (_ip, [_vp, _ip, _u8p, _sz, _ip, _vp]),
+    "bls_point_add": (_ip, [_vp, _ip, _u8p, _u8p, _vp]),
+    "bls_point_mul": (_ip, [_vp, _ip, _u8p, _u8p, _vp]),
+    "bls_point_neg": (_ip, [_vp, _ip, _u8p, _vp]),
+    "bls_multi_exp": (_ip, [_vp, _ip, _u8p, _u8p, _sz, _ip, _vp]),
+    "bls_multi_pairing": (_ip, [_vp, _u8p, _u8p, _sz, _ip, _vp]),
+    "bls_gt_mul": (_ip, [_vp, _u8p, _u8p, _vp]),
+    "bls_pairing_check_ex": (_ip, [_vp, _u8p, _u8p, _sz, _ip]),
+    "bls_comm_unique_id": (_ip, [_vp]),
+    "bls_comm_init": (_ip, [_vp, _u8p, _ip, _ip]),
+    "bls_comm_destroy": (_ip, [_vp]),
+    "bls_fav_job_check_comm": (_ip, [_vp, _ip]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -33,11 +33,20 @@ def _u8(b) -> np.ndarray:
 
 
 class Registry:
-    """HBM-resident affine pubkey table of one context."""
+    """HBM-resident affine pubkey table of one context.
+
+    The host keeps a pubkey-bytes -> index map for the keys loaded or appended through this object.  It is
+    tied to the library's registry generation (``bls_registry_generation``, bumped whenever any caller
+    replaces the device table): after a replacement by another object or by ``generate()``, lookups return
+    None instead of indices that now name other keys."""
 
     def __init__(self, ctx: _native.Context | None = None):
         self.ctx = ctx or _native.context()
         self._index: dict[bytes, int] = {}  # pubkey bytes -> first registry index (host-side lookup)
+        self._gen = None  # library registry generation the map belongs to
+
+    def _generation(self) -> int:
+        return int(self.ctx.lib.bls_registry_generation(self.ctx.h))
 
     def _remember(self, buf: np.ndarray, first: int) -> None:
         raw = buf.tobytes()
@@ -52,9 +61,10 @@ class Registry:
         n = buf.size // 48
         valid = np.zeros(n, dtype=np.uint8)
         c = self.ctx
+        self._index, self._gen = {}, None
         c.check(c.lib.bls_registry_load(c.h, buf.tobytes(), n, _ptr(valid)))
-        self._index = {}
         self._remember(buf, 0)
+        self._gen = self._generation()
         return valid
 
     def append(self, pubkeys48: bytes | np.ndarray) -> np.ndarray:
@@ -69,15 +79,24 @@ class Registry:
         valid = np.zeros(n, dtype=np.uint8)
         c = self.ctx
         c.check(c.lib.bls_registry_append(c.h, buf.tobytes(), n, _ptr(valid)))
-        self._remember(buf, first)
+        if self._gen is not None and self._gen == self._generation():
+            self._remember(buf, first)
         return valid
 
+    def _current(self) -> bool:
+        return self._gen is not None and self._gen == self._generation()
+
     def index_of(self, pubkey48: bytes) -> int | None:
-        """Registry index of a compressed pubkey loaded or appended through this object, else None."""
+        """Registry index of a compressed pubkey loaded or appended through this object, else None (also
+        None once the device table was replaced)."""
+        if not self._current():
+            return None
         return self._index.get(bytes(pubkey48))
 
     def indices(self, pubkeys) -> np.ndarray | None:
-        """u32 registry indices of every key, or None if any key is not resident."""
+        """u32 registry indices of every key, or None if any key is not resident (or the map is stale)."""
+        if not self._current():
+            return None
         out = np.empty(len(pubkeys), dtype=np.uint32)
         for i, pk in enumerate(pubkeys):
             k = self._index.get(bytes(pk))
@@ -87,11 +106,17 @@ class Registry:
         return out
 
     def generate(self, n: int, first_sk: int = 1, want_bytes: bool = False):
-        """Synthetic registry pk_i = (first_sk + i)*G1 built on the device (benchmarks)."""
+        """Synthetic registry pk_i = (first_sk + i)*G1 built on the device (benchmarks).  With want_bytes the
+        compressed keys are returned and the pubkey -> index map covers them."""
         c = self.ctx
         out = ctypes.create_string_buffer(48 * n) if want_bytes else None
+        self._index, self._gen = {}, None
         c.check(c.lib.bls_registry_generate(c.h, first_sk, n, out))
-        return out.raw if want_bytes else None
+        if want_bytes:
+            self._remember(np.frombuffer(out.raw, dtype=np.uint8), 0)
+            self._gen = self._generation()
+            return out.raw
+        return None
 
     def __len__(self):
         return int(self.ctx.lib.bls_registry_size(self.ctx.h))
@@ -133,18 +158,18 @@ def verify_batch(indices: np.ndarray, msgs32, sigs96, ctx=None) -> np.ndarray:
 def aggregate_verify_batch(pubkeys, messages, signatures, ctx=None) -> np.ndarray:
     """B AggregateVerify calls -> bool array.  pubkeys[b] / messages[b]: item b's lists of 48-byte keys
     and messages (any lengths, equal list lengths); signatures[b]: 96 bytes.  An item whose lists differ
-    in length is False (E/utils/bls.py:154-164 returns False on any exception), the rest are checked in
-    one batch (bls_aggregate_verify_batch)."""
+    in length, or with a key other than 48 bytes or a signature other than 96, is False
+    (E/utils/bls.py:154-164 returns False on any exception); the rest are checked in one batch
+    (bls_aggregate_verify_batch)."""
     c = ctx or _native.context()
     B = len(signatures)
     if len(pubkeys) != B or len(messages) != B:
         raise ValueError("need one pubkey list, one message list and one signature per item")
-    good = np.array([len(p) == len(m) and len(bytes(s)) == 96 for p, m, s in zip(pubkeys, messages, signatures)])
+    good = np.array([len(p) == len(m) and len(bytes(s)) == 96 and all(len(bytes(k)) == 48 for k in p)
+                     for p, m, s in zip(pubkeys, messages, signatures)], dtype=bool)
     lens = [len(p) if g else 0 for p, g in zip(pubkeys, good)]
     io = offsets_from_lengths(lens)
     flat_pk = [bytes(k) for p, g in zip(pubkeys, good) if g for k in p]
-    if any(len(k) != 48 for k in flat_pk):
-        raise ValueError("pubkeys must be 48 bytes")
     flat_m = [bytes(m) for ms, g in zip(messages, good) if g for m in ms]
     mo = offsets_from_lengths([len(m) for m in flat_m])
     sigs = b"".join(bytes(s) if g else bytes(96) for s, g in zip(signatures, good))
@@ -337,12 +362,20 @@ class ResidentFavBatch:
         c.check(c.lib.bls_fav_job_finish_dev(c.h, job, 1 if batch_ok else 0, self.outs[job].ptr))
         self.last_job = job
 
-    def run_pipelined(self, seeds, exchange=None, depth: int = FAV_DEPTH) -> list:
+    def job_check_comm(self, job: int) -> bool:
+        """RCCL all-gather of the job's device-resident partial + the product's final exponentiation
+        (bls_fav_job_check_comm; the context's communicator must be initialised: dist.init_comm)."""
+        c = self.ctx
+        return c.check(c.lib.bls_fav_job_check_comm(c.h, job)) == 1
+
+    def run_pipelined(self, seeds, exchange=None, depth: int = FAV_DEPTH, comm: bool = False) -> list:
         """One pass over the batch per seed with up to `depth` passes in flight:
         pass k+1.. are submitted before pass k is final-exponentiated (their
-        front kernels overlap pass k's tail).  exchange(partial) -> concatenated
-        partials of all ranks (multi-GPU all-gather); every pass is complete
-        (verdicts written) on return."""
+        front kernels overlap pass k's tail).  Multi-GPU: comm=True exchanges
+        the partials inside the library over RCCL (bls_fav_job_check_comm);
+        otherwise exchange(partial) -> concatenated partials of all ranks (a
+        host-side all-gather, e.g. gloo in the CPU tests).  Every pass is
+        complete (verdicts written) on return."""
         seeds = list(seeds)
         depth = max(1, min(depth, FAV_JOBS))
         oks = []
@@ -350,8 +383,11 @@ class ResidentFavBatch:
             self.submit(k % FAV_JOBS, seeds[k])
         for k in range(len(seeds)):
             job = k % FAV_JOBS
-            part = self.job_partial(job)
-            ok = self.job_check(job, exchange(part) if exchange else part)
+            if comm:
+                ok = self.job_check_comm(job)
+            else:
+                part = self.job_partial(job)
+                ok = self.job_check(job, exchange(part) if exchange else part)
             self.job_finish(job, ok)
             oks.append(ok)
             if k + depth < len(seeds):

@@ -23,10 +23,28 @@ Every set's verdict equals the per-call verdict of ``bls_mi355x.bls``
 a collector for the duration of a ``with`` block -- e.g. one
 ``state_transition`` -- and raises ``AssertionError`` at exit if any recorded
 signature is invalid, which is the spec's outcome for that block.
+
+Only calls whose result is *asserted* are deferred.  The spec asserts most
+verify results (``assert bls.Verify(...)`` in process_randao, exits, slashings;
+``assert is_valid_indexed_attestation(...)`` -> ``return
+bls.FastAggregateVerify(...)``), and a failed assert rejects the whole block
+whether it fires at the call or at the end of the block.  But some sites
+*branch* on the result: ``apply_deposit``'s ``if bls.Verify(...)``
+(specs/phase0/beacon-chain.md:2055) and Electra's ``if
+is_valid_deposit_signature(...)`` (specs/electra/beacon-chain.md:932,1555):
+an invalid proof of possession there skips the deposit and the block stays
+valid (test_process_deposit.py:255-287).  Returning a recorded True there
+would apply the deposit and then reject the block.  So ``try_defer`` looks at
+the caller's bytecode: the call is deferred only if its value flows, through
+``return`` statements only, into an ``assert`` (``POP_JUMP_IF_TRUE`` followed
+by ``LOAD_ASSERTION_ERROR``); any other use -- ``if``, ``not``, a comparison,
+an assignment -- runs the call at once and returns its real verdict.
 """
 from __future__ import annotations
 
 import contextlib
+import dis
+import sys
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -34,6 +52,39 @@ import numpy as np
 from . import batch as _batch
 
 FAV, VERIFY, AV = "fav", "verify", "av"
+
+_CODE_INDEX: dict = {}  # code object -> (instructions, {offset: position})
+
+
+def _next_ops(code, lasti: int, k: int = 2) -> list[str]:
+    """Opnames of the k instructions after the one at byte offset `lasti` ([] if unknown)."""
+    ent = _CODE_INDEX.get(code)
+    if ent is None:
+        ins = list(dis.get_instructions(code))
+        ent = (ins, {x.offset: i for i, x in enumerate(ins)})
+        _CODE_INDEX[code] = ent
+    ins, pos = ent
+    i = pos.get(lasti)
+    if i is None:
+        return []
+    return [x.opname for x in ins[i + 1: i + 1 + k]]
+
+
+def result_is_asserted(frame) -> bool:
+    """True iff the value returned to `frame` by the call it is executing reaches an ``assert`` through
+    ``return`` statements only (walking up the callers)."""
+    depth = 0
+    while frame is not None and depth < 32:
+        ops = _next_ops(frame.f_code, frame.f_lasti)
+        if not ops:
+            return False
+        if ops[0] == "RETURN_VALUE":
+            frame = frame.f_back
+            depth += 1
+            continue
+        return (ops[0].startswith("POP_JUMP") and ops[0].endswith("IF_TRUE") and len(ops) > 1
+                and ops[1] == "LOAD_ASSERTION_ERROR")
+    return False
 
 
 @dataclass
@@ -57,6 +108,17 @@ class SignatureSets:
         self.registry = registry
         self.ctx = ctx
         self.sets: list[_Set] = []
+        self.eager = 0  # verify calls inside deferred() that ran at once (result not asserted)
+
+    def try_defer(self, kind: str, args) -> bool:
+        """Called by the shim's Verify / FastAggregateVerify / AggregateVerify (bls.py ``_defer``): record the
+        call and return True when its result is only asserted; otherwise False (the shim verifies at once)."""
+        shim_fn = sys._getframe(2)  # try_defer <- bls._defer <- bls.Verify / ...
+        if not result_is_asserted(shim_fn.f_back):
+            self.eager += 1
+            return False
+        {VERIFY: self.add_verify, FAV: self.add_fast_aggregate_verify, AV: self.add_aggregate_verify}[kind](*args)
+        return True
 
     def __len__(self):
         return len(self.sets)
@@ -65,9 +127,16 @@ class SignatureSets:
         self.sets.append(s)
         return len(self.sets) - 1
 
+    @staticmethod
+    def _wellformed(s: _Set) -> _Set:
+        """Keys other than 48 bytes or a signature other than 96 bytes: False, as the per-call path returns."""
+        if len(s.signature) != 96 or any(k is not None and len(k) != 48 for k in s.pubkeys):
+            return _Set(s.kind, malformed=True)
+        return s
+
     def add_fast_aggregate_verify(self, pubkeys, message, signature) -> int:
         try:
-            return self._add(_Set(FAV, [_b(k) for k in pubkeys], [_b(message)], _b(signature)))
+            return self._add(self._wellformed(_Set(FAV, [_b(k) for k in pubkeys], [_b(message)], _b(signature))))
         except Exception:
             return self._add(_Set(FAV, malformed=True))
 
@@ -75,19 +144,21 @@ class SignatureSets:
         """Registry indices instead of key bytes (is_valid_indexed_attestation already holds them)."""
         try:
             idx = np.ascontiguousarray(indices, dtype=np.uint32)
-            return self._add(_Set(FAV, [None] * idx.size, [_b(message32)], _b(signature), indices=idx))
+            return self._add(self._wellformed(_Set(FAV, [None] * idx.size, [_b(message32)], _b(signature),
+                                                   indices=idx)))
         except Exception:
             return self._add(_Set(FAV, malformed=True))
 
     def add_verify(self, pubkey, message, signature) -> int:
         try:
-            return self._add(_Set(VERIFY, [_b(pubkey)], [_b(message)], _b(signature)))
+            return self._add(self._wellformed(_Set(VERIFY, [_b(pubkey)], [_b(message)], _b(signature))))
         except Exception:
             return self._add(_Set(VERIFY, malformed=True))
 
     def add_aggregate_verify(self, pubkeys, messages, signature) -> int:
         try:
-            return self._add(_Set(AV, [_b(k) for k in pubkeys], [_b(m) for m in messages], _b(signature)))
+            return self._add(self._wellformed(_Set(AV, [_b(k) for k in pubkeys], [_b(m) for m in messages],
+                                                   _b(signature))))
         except Exception:
             return self._add(_Set(AV, malformed=True))
 
@@ -152,10 +223,11 @@ class SignatureSets:
 
 @contextlib.contextmanager
 def deferred(registry: _batch.Registry | None = None, ctx=None, check: bool = True):
-    """Within the block, ``bls_mi355x.bls.Verify/FastAggregateVerify/AggregateVerify`` record their
-    arguments into a ``SignatureSets`` and return True; at exit the sets are verified in batches and,
-    with ``check``, an AssertionError names the first invalid one.  Yields the collector (its
-    ``results`` attribute holds the verdicts after the block)."""
+    """Within the block, ``bls_mi355x.bls.Verify/FastAggregateVerify/AggregateVerify`` calls whose result is
+    asserted record their arguments into a ``SignatureSets`` and return True (every other call runs at once,
+    see the module docstring); at exit the sets are verified in batches and, with ``check``, an
+    AssertionError names the first invalid one.  Yields the collector (its ``results`` attribute holds the
+    verdicts after the block)."""
     from . import bls as shim
 
     sets = SignatureSets(registry, ctx)

@@ -9,6 +9,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/blsmi355x.h"
 #include "bls_kernels.h"
 
@@ -19,7 +21,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
+  S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
@@ -29,6 +31,8 @@ enum Slot {
   S_SZ_A, S_SZ_B, S_SZ_C, S_SZ_Z,
   // KZG pieces
   S_KZ_IN, S_KZ_P, S_KZ_Q, S_KZ_OK, S_KZ_OK2, S_KZ_F, S_KZ_FT, S_KZ_S, S_KZ_J, S_KZ_OUT,
+  // curve objects (bls_g1_* / bls_g2_* / bls_multi_exp / bls_multi_pairing / bls_gt_mul)
+  S_PT_IN, S_PT_A, S_PT_OK, S_PT_TMP, S_PT_OUT,
   NSLOT
 };
 
@@ -67,11 +71,14 @@ struct bls_ctx {
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
   std::string err;
-  // registry (HBM resident)
-  G1A* reg = nullptr;
-  uint8_t* reg_ok = nullptr;
+  // registry (HBM resident): 96-B RegKey records, validity in x's top bit
+  RegKey* reg = nullptr;
   size_t reg_n = 0;
   size_t reg_cap = 0;  // entries allocated (bls_registry_append grows it)
+  uint64_t reg_gen = 0;  // bumped whenever the table is replaced (load / generate)
+  // multi-GPU exchange of FAV partials (bls_comm_*): one RCCL communicator
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 1;
   // per-kernel hipEvent timing of the FAV path (bls_profile_*)
   bool prof_on = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -249,16 +256,11 @@ struct JobScope {
   if ((job) < 0 || (job) >= ctx->njobs) return BLS_E_ARG;     \
   JobScope job_scope_(ctx, job)
 
-// Hardware-queue policy (see bls_mi355x/_native.py hw_queue_policy): the
-// FAV pipeline keeps BLS_FAV_JOBS x 3 streams busy, and with HIP's default of
-// 4 hardware queues a long lane kernel blocks the streams sharing its queue.
-// Applied when the library is loaded, i.e. before this library's first HIP
-// call; a host that initialised HIP earlier keeps its own setting.
-__attribute__((constructor)) static void bls_hw_queue_policy() {
-  if (getenv("BLSMI355X_KEEP_HW_QUEUES")) return;
-  const char* v = getenv("GPU_MAX_HW_QUEUES");
-  if (!v || atoi(v) < 20) setenv("GPU_MAX_HW_QUEUES", "20", 1);
-}
+// Hardware queues: the FAV pipeline keeps up to BLS_FAV_JOBS_INIT x 3 streams
+// busy; with HIP's default of 4 hardware queues a long lane kernel blocks the
+// streams sharing its queue.  The library does NOT change the process
+// environment: the host sets GPU_MAX_HW_QUEUES before HIP starts
+// (the Python shim does so only when it is unset).
 
 extern "C" {
 
@@ -316,6 +318,7 @@ int bls_ctx_create(int device, bls_ctx** out) {
 void bls_ctx_destroy(bls_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (Job& J : ctx->jobs) job_destroy(J);
   for (auto& p : ctx->prof_pending) ctx->prof_pool.push_back(p.second);
   for (auto& p : ctx->prof_pool) {
@@ -323,7 +326,6 @@ void bls_ctx_destroy(bls_ctx* ctx) {
     (void)hipEventDestroy(p.second);
   }
   if (ctx->reg) (void)hipFree(ctx->reg);
-  if (ctx->reg_ok) (void)hipFree(ctx->reg_ok);
   delete ctx;
 }
 
@@ -340,9 +342,80 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
   return 0;
 }
 
+// Per-call CoreVerify over n keys (n = 1: Verify, E/utils/bls.py:141-151;
+// n > 1: FastAggregateVerify, :167-177), on the three streams of job 0:
+//   stream2: hash_to_G2(msg) (lane SSWU + wave-program isogeny / cofactor phases)
+//   stream3: signature decode + G2 subgroup check
+//   stream1: KeyValidate of every key (+ their sum)
+// then the two-pair Miller product (k_miller2_vm) and one final-exponentiation
+// check.  Every chain that can be spread over a workgroup is (the h2c and
+// pairing phases); only the square roots and subgroup checks run one lane each.
+static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
+                          const uint8_t* sig96) {
+  Job& J = *ctx->j;
+  hipStream_t st = J.stream, st2 = J.stream2, st3 = J.stream3;
+  uint8_t* d_in;
+  G1A *keys, *P;
+  G2A* Q;
+  int *ok, *d_r;
+  G1J *tmp, *apk;
+  Fp* U;
+  Fd* hf;
+  int* flag;
+  Fp12* f;
+  uint64_t* d_offs;
+  const size_t in_bytes = 48 * n + 96 + msg_len;
+  SCR(S_IN0, in_bytes + 16, d_in);
+  SCR(S_OFFS, 2, d_offs);
+  SCR(S_G1A, n, keys);
+  SCR(S_OK, n + 2, ok);  // key verdicts | sig verdict | live
+  SCR(S_RP, 2, P);
+  SCR(S_G2A, 2, Q);
+  SCR(S_G1J_T, 1024, tmp);
+  SCR(S_G1J, 1, apk);
+  SCR(S_AV_U, 8, U);
+  SCR(S_AV_HCF, h2c_scratch_fd(1), hf);
+  SCR(S_AV_FLAG, 1, flag);
+  SCR(S_F, 1, f);
+  SCR(S_INT, 4, d_r);
+  uint8_t* d_pk = d_in;
+  uint8_t* d_sig = d_in + 48 * n;
+  uint8_t* d_msg = d_in + 48 * n + 96;
+  const uint64_t offs[2] = {0, msg_len};
+  CK(h2d(ctx, d_pk, pks48, 48 * n));
+  CK(h2d(ctx, d_sig, sig96, 96));
+  CK(h2d(ctx, d_msg, msg, msg_len));
+  CK(h2d(ctx, d_offs, offs, sizeof offs));
+  HIPCK(hipEventRecord(J.ev_fork, st));
+  HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
+  HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
+  LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, U, hf, Q, flag));
+  HIPCK(hipEventRecord(J.ev_join, st2));
+  LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
+  HIPCK(hipEventRecord(J.ev_sig, st3));
+  LK(launch_key_validate(st, d_pk, n, keys, ok));
+  if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
+  HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
+  LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
+  HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
+  LK(launch_miller2(st, P, Q, nullptr, 2, f));  // rejected inputs are identities here; `live` decides
+  PROF(7, launch_final_check_wave(st, f, 1, d_r));
+  int r[2] = {0, 0};
+  HIPCK(hipMemcpyAsync(&r[0], ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCK(hipMemcpyAsync(&r[1], d_r, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCK(hipStreamSynchronize(st));
+  return (r[0] && r[1]) ? 1 : 0;
+}
+
+static bool percall_lane() {  // A/B knob: the previous one-lane kernels
+  static const bool v = getenv("BLS_PERCALL") && !strcmp(getenv("BLS_PERCALL"), "lane");
+  return v;
+}
+
 int bls_verify(bls_ctx* ctx, const uint8_t* pk48, const uint8_t* msg, size_t msg_len, const uint8_t* sig96) {
   API_ENTER(ctx);
   if (!pk48 || !sig96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
+  if (!percall_lane()) return verify_percall(ctx, pk48, 1, msg, msg_len, sig96);
   uint8_t* d;
   int* d_r;
   SCR(S_IN0, 48 + 96 + msg_len, d);
@@ -361,6 +434,7 @@ int bls_fast_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, cons
   API_ENTER(ctx);
   if ((!pks48 && n) || !sig96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
   if (n == 0) return 0;
+  if (!percall_lane()) return verify_percall(ctx, pks48, n, msg, msg_len, sig96);
   G1A* a;
   int* ok;
   int v = validate_pks(ctx, pks48, n, &a, &ok);
@@ -581,28 +655,42 @@ int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8
 }
 
 // ------------------------------------------------------------- registry --
+// Decode + KeyValidate n keys into reg[first ..] (valid[] = the verdicts).
+static int registry_fill(bls_ctx* ctx, const uint8_t* pks48, size_t n, size_t first, uint8_t* out_valid) {
+  uint8_t *d_in, *d_valid;
+  G1A* d_a;
+  int* d_ok;
+  SCR(S_IN0, 48 * n, d_in);
+  SCR(S_G1A, n, d_a);
+  SCR(S_OK, n, d_ok);
+  SCR(S_IN3, n, d_valid);
+  CK(h2d(ctx, d_in, pks48, 48 * n));
+  LK(launch_key_validate(ctx->j->stream, d_in, n, d_a, d_ok));
+  LK(launch_reg_pack(ctx->j->stream, d_a, d_ok, n, ctx->reg + first, d_valid));
+  if (out_valid) CK(d2h(ctx, out_valid, d_valid, n));
+  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  return 0;
+}
+
+// A new registry replaces the old one: wait for every job's batches that may
+// still read it.
+static int registry_replace(bls_ctx* ctx, size_t n) {
+  HIPCK(hipDeviceSynchronize());
+  if (ctx->reg) HIPCK(hipFree(ctx->reg));
+  ctx->reg = nullptr;
+  ctx->reg_n = 0;
+  ctx->reg_gen++;
+  HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(RegKey)));
+  ctx->reg_cap = n ? n : 1;
+  return 0;
+}
+
 int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid) {
   API_ENTER(ctx);
   if (!pks48 && n) return BLS_E_ARG;
   if (n > 0xffffffffu) return BLS_E_ARG;
-  HIPCK(hipStreamSynchronize(ctx->j->stream));
-  if (ctx->reg) HIPCK(hipFree(ctx->reg));
-  if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
-  ctx->reg = nullptr;
-  ctx->reg_ok = nullptr;
-  ctx->reg_n = 0;
-  HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(G1A)));
-  HIPCK(hipMalloc(&ctx->reg_ok, n ? n : 1));
-  ctx->reg_cap = n ? n : 1;
-  uint8_t* d_in;
-  int* d_ok;
-  SCR(S_IN0, 48 * n, d_in);
-  SCR(S_OK, n, d_ok);
-  CK(h2d(ctx, d_in, pks48, 48 * n));
-  LK(launch_key_validate(ctx->j->stream, d_in, n, ctx->reg, d_ok));
-  LK(launch_status_to_u8(ctx->j->stream, d_ok, n, ctx->reg_ok));
-  if (out_valid) CK(d2h(ctx, out_valid, ctx->reg_ok, n));
-  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  CK(registry_replace(ctx, n));
+  if (n) CK(registry_fill(ctx, pks48, n, 0, out_valid));
   ctx->reg_n = n;
   return 1;
 }
@@ -617,30 +705,17 @@ int bls_registry_append(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* o
     HIPCK(hipDeviceSynchronize());  // batches in flight on any job read the old table
     size_t cap = ctx->reg_cap + ctx->reg_cap / 4;
     if (cap < need) cap = need;
-    G1A* nreg;
-    uint8_t* nok;
-    HIPCK(hipMalloc(&nreg, cap * sizeof(G1A)));
-    HIPCK(hipMalloc(&nok, cap));
+    RegKey* nreg;
+    HIPCK(hipMalloc(&nreg, cap * sizeof(RegKey)));
     if (ctx->reg_n) {
-      HIPCK(hipMemcpyAsync(nreg, ctx->reg, ctx->reg_n * sizeof(G1A), hipMemcpyDeviceToDevice, ctx->j->stream));
-      HIPCK(hipMemcpyAsync(nok, ctx->reg_ok, ctx->reg_n, hipMemcpyDeviceToDevice, ctx->j->stream));
+      HIPCK(hipMemcpyAsync(nreg, ctx->reg, ctx->reg_n * sizeof(RegKey), hipMemcpyDeviceToDevice, ctx->j->stream));
       HIPCK(hipStreamSynchronize(ctx->j->stream));
     }
     if (ctx->reg) HIPCK(hipFree(ctx->reg));
-    if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
     ctx->reg = nreg;
-    ctx->reg_ok = nok;
     ctx->reg_cap = cap;
   }
-  uint8_t* d_in;
-  int* d_ok;
-  SCR(S_IN0, 48 * n, d_in);
-  SCR(S_OK, n, d_ok);
-  CK(h2d(ctx, d_in, pks48, 48 * n));
-  LK(launch_key_validate(ctx->j->stream, d_in, n, ctx->reg + ctx->reg_n, d_ok));
-  LK(launch_status_to_u8(ctx->j->stream, d_ok, n, ctx->reg_ok + ctx->reg_n));
-  if (out_valid) CK(d2h(ctx, out_valid, ctx->reg_ok + ctx->reg_n, n));
-  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  CK(registry_fill(ctx, pks48, n, ctx->reg_n, out_valid));
   ctx->reg_n = need;
   return 1;
 }
@@ -650,25 +725,19 @@ size_t bls_registry_size(bls_ctx* ctx) { return ctx ? ctx->reg_n : 0; }
 int bls_registry_generate(bls_ctx* ctx, uint64_t first_sk, size_t n, uint8_t* out_pks48) {
   API_ENTER(ctx);
   if (n > 0xffffffffu || first_sk == 0 || first_sk + n < first_sk || first_sk + n >= (1ull << 62)) return BLS_E_ARG;
-  HIPCK(hipStreamSynchronize(ctx->j->stream));
-  if (ctx->reg) HIPCK(hipFree(ctx->reg));
-  if (ctx->reg_ok) HIPCK(hipFree(ctx->reg_ok));
-  ctx->reg = nullptr;
-  ctx->reg_ok = nullptr;
-  ctx->reg_n = 0;
-  HIPCK(hipMalloc(&ctx->reg, (n ? n : 1) * sizeof(G1A)));
-  HIPCK(hipMalloc(&ctx->reg_ok, n ? n : 1));
-  ctx->reg_cap = n ? n : 1;
+  CK(registry_replace(ctx, n));
   G1J* tmp;
   uint8_t* d_out = nullptr;
   SCR(S_G1J_T, n, tmp);
   if (out_pks48) SCR(S_IN0, 48 * n, d_out);
-  LK(launch_registry_generate(ctx->j->stream, first_sk, n, tmp, ctx->reg, ctx->reg_ok, d_out));
+  LK(launch_registry_generate(ctx->j->stream, first_sk, n, tmp, ctx->reg, d_out));
   if (out_pks48) CK(d2h(ctx, out_pks48, d_out, 48 * n));
   HIPCK(hipStreamSynchronize(ctx->j->stream));
   ctx->reg_n = n;
   return 1;
 }
+
+uint64_t bls_registry_generation(bls_ctx* ctx) { return ctx ? ctx->reg_gen : 0; }
 
 int bls_profile_enable(bls_ctx* ctx, int on) {
   API_ENTER(ctx);
@@ -703,7 +772,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     ctx->err = "no registry loaded";
     return BLS_E_NOREG;
   }
-  int *status, *flag, *dstat;
+  int *status, *gstat, *flag, *dstat;
   G1P *apka, *rpj;
   G1A* rP;
   G2A *sig, *H, *saff;
@@ -714,6 +783,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   uint32_t* msmu;
   uint8_t* d_seed;
   SCR(S_STATUS, B + 1, status);
+  SCR(S_GSTAT, B, gstat);
   SCR(S_APKA, B, apka);
   SCR(S_SIG, B, sig);
   SCR(S_RP, B + 1, rP);
@@ -756,22 +826,25 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   HIPCK(hipEventRecord(ctx->j->ev_join, st2));
   PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
   HIPCK(hipEventRecord(ctx->j->ev_sig, st3));
-  PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, ctx->reg_ok, (uint32_t)ctx->reg_n, apka, status));
+  PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, (uint32_t)ctx->reg_n, apka, gstat));
   HIPCK(hipEventRecord(ctx->j->ev_gather, st));
   // The MSM covers every decoded signature of a valid aggregate key, before
   // the subgroup checks: a decodable signature outside G2 stays in S, so the
-  // batch check fails and fav_finish re-checks every item individually.
+  // batch check fails and fav_finish re-checks every item individually.  It
+  // reads only gstat (gather) and dstat (decode), which no kernel writes
+  // after ev_gather / ev_sig; the subgroup verdicts go to `status`, written on
+  // stream1 while the MSM runs.
   HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_gather, 0));
   {
     ProfScope ps_(ctx, 11, st3);
-    LK(launch_msm(st3, B, status, dstat, rsc, sig, msmu, msmf, saff));
+    LK(launch_msm(st3, B, gstat, dstat, rsc, sig, msmu, msmf, saff));
     hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, rP + B);
     LK(hipGetLastError());
     LK(launch_miller_wave(st3, rP + B, saff, nullptr, 1, f + B + 1));
   }
   HIPCK(hipEventRecord(ctx->j->ev_msm, st3));
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_sig, 0));
-  PROF(10, launch_sig_vm(st, B, status, dstat, apka, sig, rsc, rpj, rP));
+  PROF(10, launch_sig_vm(st, B, gstat, status, dstat, apka, sig, rsc, rpj, rP));
   // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_join, 0));
   static const bool ml_vm = getenv("BLS_ML_VM") != nullptr;  // A/B knob: wave-program Miller (2 pairs per f)
@@ -1168,6 +1241,190 @@ int bls_g1_multi_exp(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* scalars3
   return 1;
 }
 
+// ------------------------------------------------------- curve objects --
+// (E/utils/bls.py:239-392: arkworks G1Point / G2Point / GT under fastest_bls)
+static int pt_width(int group) { return group == 1 ? 48 : group == 2 ? 96 : 0; }
+
+int bls_point_decode(bls_ctx* ctx, int group, const uint8_t* in, size_t n, int subgroup_check, uint8_t* out_ok) {
+  API_ENTER(ctx);
+  const int W = pt_width(group);
+  if (!W || (n && !in)) return BLS_E_ARG;
+  if (!n) return 1;
+  uint8_t* d_in;
+  void* d_a;
+  int* d_ok;
+  SCR(S_PT_IN, (size_t)W * n, d_in);
+  SCR(S_PT_A, (group == 1 ? sizeof(G1A) : sizeof(G2A)) * n, *(uint8_t**)&d_a);
+  SCR(S_PT_OK, n, d_ok);
+  CK(h2d(ctx, d_in, in, (size_t)W * n));
+  LK(launch_pt_decode(ctx->j->stream, group, d_in, n, subgroup_check ? 1 : 0, d_a, d_ok));
+  std::vector<int> ok(n);
+  CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
+  int all = 1;
+  for (size_t i = 0; i < n; i++) {
+    if (out_ok) out_ok[i] = ok[i] ? 1 : 0;
+    if (!ok[i]) all = 0;
+  }
+  return all;
+}
+
+static int pt_binop(bls_ctx* ctx, int group, const uint8_t* a, const uint8_t* b, const uint8_t* k32, int op,
+                    uint8_t* out) {
+  const int W = pt_width(group);
+  uint8_t* d;
+  int* d_ok;
+  SCR(S_PT_IN, 2 * (size_t)W + 32 + W, d);
+  SCR(S_PT_OK, 1, d_ok);
+  CK(h2d(ctx, d, a, W));
+  if (op == 0) CK(h2d(ctx, d + W, b, W));
+  else CK(h2d(ctx, d + 2 * W, k32, 32));
+  LK(launch_pt_binop(ctx->j->stream, group, d, d + W, d + 2 * W, op, d + 2 * W + 32, d_ok));
+  int ok = 0;
+  CK(d2h(ctx, &ok, d_ok, sizeof ok));
+  if (!ok) return 0;
+  CK(d2h(ctx, out, d + 2 * W + 32, W));
+  return 1;
+}
+
+int bls_point_add(bls_ctx* ctx, int group, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  API_ENTER(ctx);
+  if (!pt_width(group) || !a || !b || !out) return BLS_E_ARG;
+  return pt_binop(ctx, group, a, b, nullptr, 0, out);
+}
+
+int bls_point_mul(bls_ctx* ctx, int group, const uint8_t* p, const uint8_t* k32, uint8_t* out) {
+  API_ENTER(ctx);
+  if (!pt_width(group) || !p || !k32 || !out) return BLS_E_ARG;
+  return pt_binop(ctx, group, p, nullptr, k32, 1, out);
+}
+
+// -P of a compressed point is the same encoding with the sign flag flipped
+// (the identity and points with y = 0 -- none exist on E1 / E2 -- are their own
+// negation).  Byte logic only; the encoding is validated on the device first.
+int bls_point_neg(bls_ctx* ctx, int group, const uint8_t* p, uint8_t* out) {
+  const int W = pt_width(group);
+  if (!W || !p || !out) return BLS_E_ARG;
+  uint8_t ok = 0;
+  const int v = bls_point_decode(ctx, group, p, 1, 0, &ok);
+  if (v != 1) return v;
+  memcpy(out, p, W);
+  if (!(p[0] & 0x40)) out[0] ^= 0x20;
+  return 1;
+}
+
+int bls_multi_exp(bls_ctx* ctx, int group, const uint8_t* pts, const uint8_t* scalars32, size_t n, int subgroup_check,
+                  uint8_t* out) {
+  API_ENTER(ctx);
+  const int W = pt_width(group);
+  if (!W || (n && (!pts || !scalars32)) || !out) return BLS_E_ARG;
+  if (!n) return 0;  // the reference raises on an empty input (E/utils/bls.py:270-271)
+  hipStream_t st = ctx->j->stream;
+  uint8_t *d_in, *d_a, *d_tmp, *d_out;
+  int* d_ok;
+  SCR(S_PT_IN, ((size_t)W + 32) * n, d_in);
+  SCR(S_PT_A, (group == 1 ? sizeof(G1A) : sizeof(G2A)) * n, d_a);
+  SCR(S_PT_OK, n, d_ok);
+  SCR(S_PT_TMP, pt_msm_scratch_bytes(group, n), d_tmp);
+  SCR(S_PT_OUT, W, d_out);
+  CK(h2d(ctx, d_in, pts, (size_t)W * n));
+  CK(h2d(ctx, d_in + (size_t)W * n, scalars32, 32 * n));
+  LK(launch_pt_decode(st, group, d_in, n, subgroup_check ? 1 : 0, d_a, d_ok));
+  std::vector<int> ok(n);
+  CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
+  for (size_t i = 0; i < n; i++)
+    if (!ok[i]) return 0;
+  LK(launch_pt_msm(st, group, d_a, d_in + (size_t)W * n, n, d_tmp, d_out));
+  CK(d2h(ctx, out, d_out, W));
+  return 1;
+}
+
+// prod_i e(P_i, Q_i) after the final exponentiation, as 576 bytes
+int bls_multi_pairing(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, int subgroup_check,
+                      uint8_t* out576) {
+  API_ENTER(ctx);
+  if ((n && (!g1s48 || !g2s96)) || !out576) return BLS_E_ARG;
+  if (!n) {  // the empty product: GT one (c0.c0.c0 = 1 in the 576-byte layout)
+    memset(out576, 0, 576);
+    out576[47] = 1;
+    return 1;
+  }
+  hipStream_t st = ctx->j->stream;
+  uint8_t *d_in, *d_out;
+  G1A* P;
+  G2A* Q;
+  int *ok1, *ok2;
+  Fp12 *f, *ft, *fo;
+  SCR(S_KZ_IN, 144 * n, d_in);
+  SCR(S_KZ_P, n, P);
+  SCR(S_KZ_Q, n, Q);
+  SCR(S_KZ_OK, n, ok1);
+  SCR(S_KZ_OK2, n, ok2);
+  SCR(S_KZ_F, n, f);
+  SCR(S_KZ_FT, n / 8 + 16, ft);
+  SCR(S_FPART, 1, fo);
+  SCR(S_PT_OUT, 576, d_out);
+  CK(h2d(ctx, d_in, g1s48, 48 * n));
+  CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
+  LK(launch_pt_decode(st, 1, d_in, n, subgroup_check ? 1 : 0, P, ok1));
+  LK(launch_pt_decode(st, 2, d_in + 48 * n, n, subgroup_check ? 1 : 0, Q, ok2));
+  std::vector<int> a(n), b(n);
+  CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
+  CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
+  for (size_t i = 0; i < n; i++)
+    if (!a[i] || !b[i]) return 0;
+  LK(launch_miller_wave(st, P, Q, nullptr, n, f));  // identity pairs contribute 1
+  LK(launch_fp12_prod_vm(st, f, n, ft, fo));
+  LK(launch_gt_final_exp(st, fo, d_out));
+  CK(d2h(ctx, out576, d_out, 576));
+  return 1;
+}
+
+int bls_gt_mul(bls_ctx* ctx, const uint8_t* a576, const uint8_t* b576, uint8_t* out576) {
+  API_ENTER(ctx);
+  if (!a576 || !b576 || !out576) return BLS_E_ARG;
+  uint8_t* d;
+  SCR(S_PT_IN, 3 * 576, d);
+  CK(h2d(ctx, d, a576, 576));
+  CK(h2d(ctx, d + 576, b576, 576));
+  LK(launch_gt_mul(ctx->j->stream, d, d + 576, d + 1152));
+  CK(d2h(ctx, out576, d + 1152, 576));
+  return 1;
+}
+
+// pairing_check with the subgroup checks optional (arkworks multi_pairing on
+// already-decoded curve objects checks none)
+int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, int subgroup_check) {
+  API_ENTER(ctx);
+  if (n && (!g1s48 || !g2s96)) return BLS_E_ARG;
+  if (n == 0) return 1;  // empty product
+  hipStream_t st = ctx->j->stream;
+  uint8_t* d_in;
+  G1A* P;
+  G2A* Q;
+  int *ok1, *ok2;
+  Fp12 *f, *ft, *fo;
+  SCR(S_KZ_IN, 144 * n, d_in);
+  SCR(S_KZ_P, n, P);
+  SCR(S_KZ_Q, n, Q);
+  SCR(S_KZ_OK, n, ok1);
+  SCR(S_KZ_OK2, n, ok2);
+  SCR(S_KZ_F, n, f);
+  SCR(S_KZ_FT, n / 8 + 16, ft);
+  SCR(S_FPART, 1, fo);
+  CK(h2d(ctx, d_in, g1s48, 48 * n));
+  CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
+  LK(launch_pt_decode(st, 1, d_in, n, subgroup_check ? 1 : 0, P, ok1));
+  LK(launch_pt_decode(st, 2, d_in + 48 * n, n, subgroup_check ? 1 : 0, Q, ok2));
+  std::vector<int> a(n), b(n);
+  CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
+  CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
+  for (size_t i = 0; i < n; i++)
+    if (!a[i] || !b[i]) return 0;
+  LK(launch_miller_wave(st, P, Q, nullptr, n, f));
+  LK(launch_fp12_prod_vm(st, f, n, ft, fo));
+  return run_final_check(ctx, fo);
+}
+
 int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds) {
   API_ENTER(ctx);
   if (fe_checks) *fe_checks = ctx->j->bis_checks;
@@ -1297,6 +1554,89 @@ int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t 
 int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out) {
   JOB_ENTER(ctx, job);
   return job_finish(ctx, batch_ok, d_out);
+}
+
+// ------------------------------------------- multi-GPU exchange (RCCL) --
+// every rank reduces its shard to one 576-byte Fp12 Miller
+// partial; ncclAllGather moves the world x 576 bytes over xGMI (the transfer
+// is latency-bound, not bandwidth-bound), and every rank multiplies the
+// partials inside its final-exponentiation kernel -- no broadcast.  Fp12
+// multiplication is not an elementwise sum, so this is an all-gather, not an
+// all-reduce.
+static int nccl_fail(bls_ctx* c, ncclResult_t r, const char* where) {
+  char b[256];
+  snprintf(b, sizeof b, "%s: %s", where, ncclGetErrorString(r));
+  c->err = b;
+  return BLS_E_DEVICE;
+}
+
+int bls_comm_unique_id(uint8_t* out128) {
+  if (!out128) return BLS_E_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return BLS_E_DEVICE;
+  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+  memcpy(out128, &id, sizeof id);
+  return 0;
+}
+
+int bls_comm_init(bls_ctx* ctx, const uint8_t* uid128, int rank, int world) {
+  API_ENTER(ctx);
+  if (!uid128 || world < 1 || rank < 0 || rank >= world) return BLS_E_ARG;
+  if (ctx->comm) {
+    (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ncclUniqueId id;
+  memcpy(&id, uid128, sizeof id);
+  const ncclResult_t r = ncclCommInitRank(&ctx->comm, world, id, rank);
+  if (r != ncclSuccess) {
+    ctx->comm = nullptr;
+    return nccl_fail(ctx, r, "ncclCommInitRank");
+  }
+  ctx->comm_rank = rank;
+  ctx->comm_world = world;
+  return 0;
+}
+
+int bls_comm_destroy(bls_ctx* ctx) {
+  API_ENTER(ctx);
+  if (ctx->comm) {
+    const ncclResult_t r = ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclCommDestroy");
+  }
+  ctx->comm_rank = 0;
+  ctx->comm_world = 1;
+  return 0;
+}
+
+// All-gather job `job`'s device-resident partial (written by its submit) with
+// every rank's, on the job's stream, then the product's final exponentiation:
+// 1 / 0.  The host never sees the partials.  Every rank must call this for the
+// same jobs in the same order (one outstanding collective at a time: the call
+// waits for the verdict).
+int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
+  JOB_ENTER(ctx, job);
+  Job& J = *ctx->j;
+  if (!ctx->comm) {
+    ctx->err = "bls_comm_init was not called";
+    return BLS_E_ARG;
+  }
+  if (!J.partial_pending || !J.buf[S_BYTES].p) {
+    ctx->err = "no submitted FAV batch on this job";
+    return BLS_E_ARG;
+  }
+  const int W = ctx->comm_world;
+  uint8_t* d_all;
+  Fp12* f;
+  SCR(S_IN0, 576 * (size_t)W, d_all);
+  SCR(S_FCHK, W, f);
+  const ncclResult_t r =
+      ncclAllGather(J.buf[S_BYTES].p, d_all, 576, ncclUint8, ctx->comm, J.stream);
+  if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllGather");
+  J.partial_pending = false;  // consumed on the device (the pinned host copy is not waited for)
+  PROF(9, launch_fp12_from_bytes(J.stream, d_all, W, f));
+  return run_final_check(ctx, f, W);
 }
 
 }  // extern "C"

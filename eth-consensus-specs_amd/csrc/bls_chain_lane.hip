@@ -78,11 +78,13 @@ BLS_HD PP<F> pp_add_aff(const PP<F>& p, const F& x2, const F& y2) {
   return pp_finish(t0, t1, ln_b3(p.z), t3, t4, y3);
 }
 
-__global__ void __launch_bounds__(64) k_sig_lane(size_t B, int* status, const int* dstat, const G1P* apk,
-                                                 const G2A* sig, const uint64_t* rsc, G1P* rPj) {
+// gstat: the gather's per-item status (read-only here: the MSM on another
+// stream reads it concurrently); status: this kernel's verdict.
+__global__ void __launch_bounds__(64) k_sig_lane(size_t B, const int* gstat, int* status, const int* dstat,
+                                                 const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B) return;
-  const bool live = status[i] && dstat[i];
+  const bool live = gstat[i] && dstat[i];
   if (!live) {
     status[i] = 0;
     return;
@@ -136,11 +138,11 @@ __global__ void __launch_bounds__(64) k_g2x_lane(size_t B, Fd* hf, int src, int 
   o[5] = fd_from_fp(M.z.c1);
 }
 
-hipError_t launch_sig_lane(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk, const G2A* sig,
-                           const uint64_t* rsc, G1P* rPj) {
+hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
+                           const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_lane, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, status, dstat, apk, sig, rsc,
-                     rPj);
+  hipLaunchKernelGGL(k_sig_lane, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat, apk, sig,
+                     rsc, rPj);
   return hipGetLastError();
 }
 

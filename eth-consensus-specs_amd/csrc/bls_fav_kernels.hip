@@ -193,17 +193,21 @@ __global__ void __launch_bounds__(64) k_h2c_affine(size_t B, const int* status, 
   H[i] = h;
 }
 
+// The fallback runs as ONE 64-lane workgroup striding over the flags: its
+// inlined hash_to_g2 needs ~6 KB of private segment per lane, and the scratch
+// the runtime reserves for a dispatch grows with its grid (a launch over all
+// B items reserved ~60 MB per queue, which with 15+ hardware queues ended in
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Flags are ~never set, so the loop is
+// B / 64 flag loads.
 __global__ void __launch_bounds__(64) k_h2c_fallback(size_t B, const uint8_t* msgs32, const int* flag, G2A* H) {
-  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= B || !flag[i]) return;
-  H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_FAV, 43));
+  for (size_t i = threadIdx.x; i < B; i += 64)
+    if (flag[i]) H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_FAV, 43));
 }
 
 __global__ void __launch_bounds__(64) k_h2c_fallback_var(size_t B, const uint8_t* msgs, const uint64_t* offs,
                                                          const int* flag, G2A* H) {
-  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= B || !flag[i]) return;
-  H[i] = jac_to_aff(hash_to_g2(msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_FAV, 43));
+  for (size_t i = threadIdx.x; i < B; i += 64)
+    if (flag[i]) H[i] = jac_to_aff(hash_to_g2(msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_FAV, 43));
 }
 
 // ----------------------------------------------------------- signatures --
@@ -242,8 +246,8 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
 // subgroup check and r * apk), then the subgroup verdict and r * apk to
 // affine.  sum r_i sigma_i is the batch MSM (bls_msm.hip).
 template <int G>
-__global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const int* dstat, const G1P* apk,
-                                                 const G2A* sig, const uint64_t* rsc, G1P* rPj) {
+__global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, const int* gstat, int* status, const int* dstat,
+                                                 const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   __shared__ Fd s[WP_NCONST + G * WL_SG_STRIDE];
   __shared__ int live[G];
   __shared__ uint32_t pred[G];
@@ -253,7 +257,7 @@ __global__ void __launch_bounds__(64, 3) k_sig_vm(size_t B, int* status, const i
   uint64_t r = 0;
   if (lane < G) {
     const size_t i = i0 + lane;
-    live[lane] = i < B && status[i] && dstat[i];
+    live[lane] = i < B && gstat[i] && dstat[i];
     r = live[lane] ? rsc[i] : 0;
   }
   __syncthreads();
@@ -358,7 +362,7 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
   e = hg == 4 ? launch_h2c_phases<4>(st, B, status, U, hf, H, flag, xg)
               : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_h2c_fallback, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs32, flag, H);
+  hipLaunchKernelGGL(k_h2c_fallback, dim3(1), dim3(64), 0, st, B, msgs32, flag, H);
   return hipGetLastError();
 }
 
@@ -370,7 +374,7 @@ hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const 
   if (e != hipSuccess) return e;
   e = launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, env_int_or("BLS_XC_G", 5));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_h2c_fallback_var, dim3(nblk(B, 64)), dim3(64), 0, st, B, msgs, offs, flag, H);
+  hipLaunchKernelGGL(k_h2c_fallback_var, dim3(1), dim3(64), 0, st, B, msgs, offs, flag, H);
   return hipGetLastError();
 }
 
@@ -381,19 +385,22 @@ hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, co
   return hipGetLastError();
 }
 
-hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff,
-                         const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP) {
+hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat,
+                         const G1P* apk_aff, const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP) {
   if (!B) return hipSuccess;
   static const int sg = env_int_or("BLS_SIG_G", 1);  // 1: one lane per item; 2/4/6: wave programs
   if (sg == 1) {
-    hipError_t e = launch_sig_lane(st, B, status, dstat, apk_aff, sig, rsc, rPj);
+    hipError_t e = launch_sig_lane(st, B, gstat, status, dstat, apk_aff, sig, rsc, rPj);
     if (e != hipSuccess) return e;
   } else if (sg == 4)
-    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
+    hipLaunchKernelGGL(k_sig_vm<4>, dim3(nblk(B, 4)), dim3(64), 0, st, B, gstat, status, dstat, apk_aff, sig, rsc,
+                       rPj);
   else if (sg == 6)
-    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
+    hipLaunchKernelGGL(k_sig_vm<6>, dim3(nblk(B, 6)), dim3(64), 0, st, B, gstat, status, dstat, apk_aff, sig, rsc,
+                       rPj);
   else
-    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, status, dstat, apk_aff, sig, rsc, rPj);
+    hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, gstat, status, dstat, apk_aff, sig, rsc,
+                       rPj);
   hipLaunchKernelGGL(k_g1_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, rPj, rP);
   return hipGetLastError();
 }

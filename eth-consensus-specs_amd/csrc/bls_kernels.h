@@ -12,10 +12,14 @@ hipError_t launch_g1_compress(hipStream_t st, const G1J* in, uint8_t* out48, int
 hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96);
 hipError_t launch_verify_single(hipStream_t st, const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig, int* out);
 hipError_t launch_verify_apk(hipStream_t st, const G1J* apk, const uint8_t* msg, uint32_t len, const uint8_t* sig, int* out);
+hipError_t launch_percall_pairs(hipStream_t st, const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum,
+                                const int* sig_ok, G1A* P, int* live);
 hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst, uint32_t dst_len, G2A* out);
 hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n, uint8_t* out, int* ok);
 hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok);
-hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg, const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status);
+hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const RegKey* reg, uint32_t reg_n, G1P* apk, int* status);
+// registry entries from k_key_validate output (+ the host validity mask)
+hipError_t launch_reg_pack(hipStream_t st, const G1A* a, const int* ok, size_t n, RegKey* reg, uint8_t* valid);
 hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP, const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2);
 hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok, const G2A* sig, const uint64_t* rsc, int* status, G1A* P2, G2A* Q2);
 hipError_t launch_av_pairs(hipStream_t st, size_t total, const uint32_t* pair_item, const int* status, const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2);
@@ -33,12 +37,13 @@ hipError_t launch_status_to_u8(hipStream_t st, const int* status, size_t B, uint
 hipError_t launch_fp12_to_bytes(hipStream_t st, const Fp12* f, uint8_t* out);
 hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, Fp12* f);
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96);
-hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok, uint8_t* out48);
+hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, RegKey* reg, uint8_t* out48);
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 constexpr int HCF = 24;  // hash_to_G2 staging: Fd slots per item (bls_fav_kernels.hip, bls_chain_lane.hip)
 // one lane per item (bls_chain_lane.hip)
-hipError_t launch_sig_lane(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk, const G2A* sig,
-                           const uint64_t* rsc, G1P* rPj);
+// gstat: gather status (read-only: the MSM reads it concurrently on another stream); status: written
+hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
+                           const G2A* sig, const uint64_t* rsc, G1P* rPj);
 hipError_t launch_g2x_lane(hipStream_t st, size_t B, Fd* hf, int src, int dst);
 // hf: h2c_scratch_fd(B) Fd slots of staging between the hash_to_G2 phases
 size_t h2c_scratch_fd(size_t B);
@@ -49,8 +54,8 @@ hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const 
                            int* flag);
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat);
 // rPj: B projective scratch points (r_i apk_i before the affine conversion)
-hipError_t launch_sig_vm(hipStream_t st, size_t B, int* status, const int* dstat, const G1P* apk_aff, const G2A* sig,
-                         const uint64_t* rsc, G1P* rPj, G1A* rP);
+hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk_aff,
+                         const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP);
 size_t msm_scratch_u32(size_t B);
 size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
@@ -68,5 +73,16 @@ hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* ou
 hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out);
 hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out);
 hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out);
+
+// curve objects (bls_points.hip): group 1 = G1 (48-B encodings, G1A), 2 = G2 (96-B, G2A)
+hipError_t launch_pt_decode(hipStream_t st, int group, const uint8_t* in, size_t n, int subgroup, void* out, int* ok);
+// op 0: a + b, op 1: [k32] a; *ok = 0 if an encoding is invalid
+hipError_t launch_pt_binop(hipStream_t st, int group, const uint8_t* a, const uint8_t* b, const uint8_t* k32, int op,
+                           uint8_t* out, int* ok);
+size_t pt_msm_scratch_bytes(int group, size_t n);
+hipError_t launch_pt_msm(hipStream_t st, int group, const void* P, const uint8_t* k32, size_t n, void* tmp,
+                         uint8_t* out);
+hipError_t launch_gt_final_exp(hipStream_t st, const Fp12* f, uint8_t* out576);
+hipError_t launch_gt_mul(hipStream_t st, const uint8_t* a, const uint8_t* b, uint8_t* out);
 
 }  // namespace bls

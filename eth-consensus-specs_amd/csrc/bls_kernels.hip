@@ -119,6 +119,22 @@ __global__ void k_verify_apk(const G1J* apk, const uint8_t* msg, uint32_t msg_le
   *out = core_verify_point(a, msg, msg_len, DST_POP_DEV, 43, sig96);
 }
 
+// Per-call path (bls_verify / bls_fast_aggregate_verify): the pairs
+// (apk, H(m)) and (-G1, sigma) for k_miller2_vm.  apk is the validated key
+// (n == 1) or the sum of the validated keys; *live = 0 if any key failed
+// KeyValidate, the sum is the identity, or the signature failed its checks.
+__global__ void k_percall_pairs(const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum, const int* sig_ok,
+                                G1A* P, int* live) {
+  if (threadIdx.x || blockIdx.x) return;
+  int ok = sig_ok[0];
+  for (size_t i = 0; i < n; i++) ok = ok && key_ok[i];
+  const G1A a = n == 1 ? keys[0] : jac_to_aff(apk_sum[0]);
+  ok = ok && !a.inf;
+  P[0] = a;
+  P[1] = g1_neg_generator();
+  *live = ok;
+}
+
 __global__ void __launch_bounds__(64) k_hash_many(const uint8_t* msgs, const uint64_t* offs, size_t n,
                                                   const uint8_t* dst, uint32_t dst_len, G2A* out) {
   size_t i = gtid();
@@ -229,8 +245,8 @@ __device__ __forceinline__ G1P g1p_add(const G1P& p, const G1P& q) {
 // committees L = 16 (32 mixed additions per lane + 4 tree levels) beats 64
 // lanes (8 + 6 levels: the tree was ~45 % of the wave's time).
 template <int L>
-__global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
-                                                   const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status) {
+__global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const uint64_t* offs, size_t B,
+                                                   const RegKey* reg, uint32_t reg_n, G1P* apk, int* status) {
   constexpr int IPW = 64 / L;
   __shared__ G1P sh[64];
   __shared__ int bad[IPW];
@@ -246,10 +262,26 @@ __global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const ui
     hi = offs[b + 1];
     for (uint64_t j = lo + ln; j < hi; j += L) {
       const uint32_t k = idx[j];
-      if (k >= reg_n || !reg_ok[k]) {
+      if (k >= reg_n) {
+        mybad = 1;
+        continue;
+      }
+      // one 96-B record: six 16-B loads, x's top bit is the validity flag
+      const uint4* r = reinterpret_cast<const uint4*>(reg + k);
+      Fp x, y;
+      uint4* xv = reinterpret_cast<uint4*>(x.l);
+      uint4* yv = reinterpret_cast<uint4*>(y.l);
+      xv[0] = r[0];
+      xv[1] = r[1];
+      xv[2] = r[2];
+      yv[0] = r[3];
+      yv[1] = r[4];
+      yv[2] = r[5];
+      if (!(x.l[11] & REG_VALID)) {
         mybad = 1;
       } else {
-        acc = g1p_add_aff(acc, reg[k].x, reg[k].y);
+        x.l[11] &= ~REG_VALID;
+        acc = g1p_add_aff(acc, x, y);
       }
     }
   }
@@ -265,6 +297,19 @@ __global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const ui
     apk[b] = sh[threadIdx.x];
     status[b] = (hi > lo && !bad[sub] && !fp_is_zero(sh[threadIdx.x].z)) ? 1 : 0;
   }
+}
+
+// Registry entries from decoded keys (bls_registry_load / _append): the
+// KeyValidate verdict goes into x's spare top bit; valid[i] = 1/0 for the host.
+__global__ void __launch_bounds__(256) k_reg_pack(const G1A* a, const int* ok, size_t n, RegKey* reg, uint8_t* valid) {
+  const size_t i = gtid();
+  if (i >= n) return;
+  RegKey e{a[i].x, a[i].y};
+  const bool v = ok[i] != 0;
+  if (!v) e = RegKey{fp_zero(), fp_zero()};
+  e.x.l[11] |= v ? REG_VALID : 0u;
+  reg[i] = e;
+  valid[i] = v ? 1 : 0;
 }
 
 // (4) bisection fallback (fav_bisect in bls_capi.hip).  Per item i the two
@@ -402,7 +447,7 @@ __global__ void k_fp12_from_bytes(const uint8_t* in, size_t n, Fp12* f) {
 // walks a chunk of consecutive multiples (mixed additions of G1) and
 // normalises the chunk with one inversion (Montgomery's batch trick).
 __global__ void __launch_bounds__(64) k_registry_generate(uint64_t first, size_t n, uint32_t chunk, G1J* tmpJ,
-                                                          G1A* reg, uint8_t* reg_ok, uint8_t* out48) {
+                                                          RegKey* reg, uint8_t* out48) {
   size_t t = gtid();
   size_t lo = t * chunk;
   if (lo >= n) return;
@@ -426,8 +471,9 @@ __global__ void __launch_bounds__(64) k_registry_generate(uint64_t first, size_t
     inv = fp_mul(inv, tmpJ[i].z);
     Fp zi2 = fp_sqr(zi);
     G1A a{fp_mul(tmpJ[i].x, zi2), fp_mul(fp_mul(tmpJ[i].y, zi2), zi), false};
-    reg[i] = a;
-    reg_ok[i] = 1;
+    RegKey e{a.x, a.y};
+    e.x.l[11] |= REG_VALID;
+    reg[i] = e;
     if (out48) g1_compress(out48 + 48 * i, a);
   }
 }
@@ -488,6 +534,11 @@ hipError_t launch_verify_apk(hipStream_t st, const G1J* apk, const uint8_t* msg,
   LAUNCH(k_verify_apk, 1, 64, st, apk, msg, len, sig, out);
   return hipSuccess;
 }
+hipError_t launch_percall_pairs(hipStream_t st, const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum,
+                                const int* sig_ok, G1A* P, int* live) {
+  LAUNCH(k_percall_pairs, 1, 64, st, keys, key_ok, n, apk_sum, sig_ok, P, live);
+  return hipSuccess;
+}
 hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst,
                             uint32_t dst_len, G2A* out) {
   if (!n) return hipSuccess;
@@ -505,21 +556,21 @@ hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, ui
   LAUNCH(k_sk_to_pk_many, nblk(n, 64), 64, st, sks, n, out, ok);
   return hipSuccess;
 }
-hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const G1A* reg,
-                             const uint8_t* reg_ok, uint32_t reg_n, G1P* apk, int* status) {
+hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const RegKey* reg,
+                             uint32_t reg_n, G1P* apk, int* status) {
   if (!B) return hipSuccess;
   // lanes per aggregate: 16 while that still gives >= ~2 waves per SIMD and the
   // committees are not huge (the per-lane chains stay short), else 64
   static const int forced = getenv("BLS_GATHER_L") ? atoi(getenv("BLS_GATHER_L")) : 0;
   int L = forced ? forced : (B >= 8192 ? 16 : 64);
   if (L == 16)
-    LAUNCH(k_fav_gather<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+    LAUNCH(k_fav_gather<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else if (L == 8)
-    LAUNCH(k_fav_gather<8>, (unsigned)((B + 7) / 8), 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+    LAUNCH(k_fav_gather<8>, (unsigned)((B + 7) / 8), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else if (L == 32)
-    LAUNCH(k_fav_gather<32>, (unsigned)((B + 1) / 2), 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+    LAUNCH(k_fav_gather<32>, (unsigned)((B + 1) / 2), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else
-    LAUNCH(k_fav_gather<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_ok, reg_n, apk, status);
+    LAUNCH(k_fav_gather<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
   return hipSuccess;
 }
 hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP,
@@ -569,12 +620,17 @@ hipError_t launch_fp12_from_bytes(hipStream_t st, const uint8_t* in, size_t n, F
   LAUNCH(k_fp12_from_bytes, nblk(n, 64), 64, st, in, n, f);
   return hipSuccess;
 }
-hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, G1A* reg, uint8_t* reg_ok,
+hipError_t launch_registry_generate(hipStream_t st, uint64_t first, size_t n, G1J* tmpJ, RegKey* reg,
                                     uint8_t* out48) {
   if (!n) return hipSuccess;
   const uint32_t chunk = 32;
   size_t threads = (n + chunk - 1) / chunk;
-  LAUNCH(k_registry_generate, nblk(threads, 64), 64, st, first, n, chunk, tmpJ, reg, reg_ok, out48);
+  LAUNCH(k_registry_generate, nblk(threads, 64), 64, st, first, n, chunk, tmpJ, reg, out48);
+  return hipSuccess;
+}
+hipError_t launch_reg_pack(hipStream_t st, const G1A* a, const int* ok, size_t n, RegKey* reg, uint8_t* valid) {
+  if (!n) return hipSuccess;
+  LAUNCH(k_reg_pack, nblk(n, 256), 256, st, a, ok, n, reg, valid);
   return hipSuccess;
 }
 hipError_t launch_g2_compress_aff(hipStream_t st, const G2A* in, uint8_t* out96) {

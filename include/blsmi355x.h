@@ -90,6 +90,10 @@ int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8
  * Returns 1 or BLS_E_*. */
 int bls_registry_load(bls_ctx* ctx, const uint8_t* pks48, size_t n, uint8_t* out_valid);
 size_t bls_registry_size(bls_ctx* ctx);
+/* Generation of the registry table: bumped whenever bls_registry_load or
+ * bls_registry_generate replaces it (appends keep it).  A host-side
+ * pubkey -> index map is valid only for the generation it was built on. */
+uint64_t bls_registry_generation(bls_ctx* ctx);
 
 /* B FastAggregateVerify calls over registry indices: item b uses
  * idx[offsets[b] .. offsets[b+1]) (offsets has B+1 entries), message
@@ -151,6 +155,35 @@ int bls_pairing_check(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, 
  * BLS_E_*. */
 int bls_g1_multi_exp(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* scalars32, size_t n, uint8_t* out48);
 
+/* ---- curve objects  <- E/utils/bls.py:224-392 ---------------------------
+ * The arkworks G1Point / G2Point / GT operations of the reference's
+ * fastest_bls helpers: add (:239-246), multiply (:249-259), multi_exp
+ * (:262-296), neg (:299-306), bytes48_to_G1 / bytes96_to_G2 (unchecked decode,
+ * :367-392), G1_to_bytes48 / G2_to_bytes96 (:345-364), pairing_check
+ * (:224-236).  group: 1 = G1 (48-byte compressed), 2 = G2 (96-byte).  The
+ * identity encoding is a valid point.  Return 1 on success, 0 if an encoding
+ * is invalid (the reference raises), BLS_E_* on errors. */
+/* out_ok[i] (may be NULL) = 1 iff in[i] decodes (and, with subgroup_check, lies
+ * in G1 / G2); returns 1 iff all do. */
+int bls_point_decode(bls_ctx* ctx, int group, const uint8_t* in, size_t n, int subgroup_check, uint8_t* out_ok);
+int bls_point_add(bls_ctx* ctx, int group, const uint8_t* a, const uint8_t* b, uint8_t* out);
+/* [k] P, k a 32-byte big-endian integer (the reference reduces scalars mod r first) */
+int bls_point_mul(bls_ctx* ctx, int group, const uint8_t* p, const uint8_t* k32, uint8_t* out);
+int bls_point_neg(bls_ctx* ctx, int group, const uint8_t* p, uint8_t* out);
+/* sum_i [k_i] P_i.  n == 0 -> 0 (the reference raises, E/utils/bls.py:270-271).
+ * subgroup_check 0 = multiexp_unchecked (:280-282). */
+int bls_multi_exp(bls_ctx* ctx, int group, const uint8_t* pts, const uint8_t* scalars32, size_t n, int subgroup_check,
+                  uint8_t* out);
+/* GT.multi_pairing: prod_i e(P_i, Q_i) after the final exponentiation, as 576
+ * bytes (six Fp2 coefficients c0..c5 of the w-basis, each c0||c1 big-endian;
+ * GT one = byte 47 set).  n == 0 gives one. */
+int bls_multi_pairing(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, int subgroup_check,
+                      uint8_t* out576);
+int bls_gt_mul(bls_ctx* ctx, const uint8_t* a576, const uint8_t* b576, uint8_t* out576);
+/* pairing_check over curve objects (arkworks GT.multi_pairing(...) == GT.one(),
+ * :229): subgroup_check 0 skips the subgroup checks of bls_pairing_check. */
+int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, int subgroup_check);
+
 /* Fallback statistics of the last batch call on this context: the number of
  * batched final-exponentiation checks and bisection rounds it ran (both 0
  * when the whole-batch check passed).  Returns 0 or BLS_E_*. */
@@ -205,6 +238,21 @@ int bls_fav_job_submit_dev(bls_ctx* ctx, int job, const uint32_t* d_idx, const u
 int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576);
 int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t n);
 int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out);
+
+/* ---- multi-GPU exchange over RCCL ----------------------
+ * One communicator per context.  bls_comm_unique_id runs on one rank; its 128
+ * bytes reach the other ranks out of band (bench.py: the torchrun TCP store).
+ * bls_fav_job_check_comm replaces job_partial + host exchange + job_check: the
+ * job's 576-byte partial is all-gathered on the device (ncclAllGather over
+ * xGMI, on the job's stream), the world partials are multiplied inside the
+ * final-exponentiation kernel, and the verdict (1 / 0) returns.  Every rank
+ * calls it for the same jobs in the same order.  A failing verdict is then
+ * localised by bls_fav_job_finish_dev(..., 0, ...) on every rank: each
+ * re-checks its own partial first, so only the bad shard bisects. */
+int bls_comm_unique_id(uint8_t* out128);
+int bls_comm_init(bls_ctx* ctx, const uint8_t* uid128, int rank, int world);
+int bls_comm_destroy(bls_ctx* ctx);
+int bls_fav_job_check_comm(bls_ctx* ctx, int job);
 
 /* ---- tracing: hipEvent time per kernel of the FAV path ------------------ */
 int bls_profile_enable(bls_ctx* ctx, int on);  /* also resets the totals */

@@ -1,7 +1,11 @@
-"""world_size-2 gloo test of the multi-GPU combination protocol
-(bls_mi355x.dist): each rank holds the Miller product of its shard, the
-576-byte partials are all-gathered, every rank multiplies and final-
-exponentiates.  Partials here come from the oracle (no GPU on CPU)."""
+"""world_size-2 gloo test of the multi-GPU combination protocol (SURVEY.md
+§8(e), bls_mi355x.dist / bls_fav_job_check_comm): each rank holds the Miller
+product of its shard, the 576-byte partials are all-gathered, every rank
+multiplies and final-exponentiates; when the product fails, every rank
+re-checks its own partial first (bls_fav_job_finish_dev with batch_ok = 0),
+so only the bad shard bisects.  Partials here come from the oracle and the
+all-gather is gloo's (no GPU on CPU); the library's RCCL all-gather of the
+same bytes is exercised on the GPU (tests/test_gpu_comm.py)."""
 import os
 import socket
 
@@ -28,10 +32,20 @@ def _from_bytes(b):
                                int.from_bytes(b[96 * k + 48: 96 * k + 96], "big")) for k in range(6)])
 
 
+def _allgather(partial):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.frombuffer(bytearray(partial), dtype=torch.uint8)
+    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return b"".join(bytes(o.numpy()) for o in outs)
+
+
 def _worker(rank, world, port, tamper, q):
     import torch.distributed as dist
 
-    from bls_mi355x.dist import allgather_partials
+    from bls_mi355x.dist import shard_bounds
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -42,11 +56,15 @@ def _worker(rank, world, port, tamper, q):
     pk = O.g1_mul(O.G1_GEN, sk)
     sig = O.g2_decompress(O.Sign(sk if not (tamper and rank == 1) else sk + 1, m))
     f = O.f12_mul(O.miller_loop(pk, O.hash_to_g2(m)), O.miller_loop(O.g1_neg(O.G1_GEN), sig))
-    allp = allgather_partials(_partial_bytes(f))
+    allp = _allgather(_partial_bytes(f))
     prod = O.F12_ONE
     for k in range(world):
         prod = O.f12_mul(prod, _from_bytes(allp[576 * k: 576 * k + 576]))
-    q.put((rank, O.final_exponentiation(prod) == O.F12_ONE))
+    ok = O.final_exponentiation(prod) == O.F12_ONE
+    # a failing product: each rank re-checks its own partial (finish_dev's root re-check)
+    own_ok = True if ok else O.final_exponentiation(f) == O.F12_ONE
+    assert shard_bounds(10, rank, world) == ((0, 5), (5, 10))[rank]
+    q.put((rank, (ok, own_ok)))
     dist.destroy_process_group()
 
 
@@ -61,4 +79,4 @@ def test_two_rank_partials(tamper):
     res = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: not tamper, 1: not tamper}
+    assert res == {0: (not tamper, True), 1: (not tamper, not tamper)}  # only rank 1's shard is bad

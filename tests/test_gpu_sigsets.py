@@ -126,12 +126,50 @@ def test_registry_append_and_lookup(b):
     assert list(out) == [True]
 
 
+# Spec-shaped call sites compiled from source like the generated spec modules (pytest rewrites the asserts of
+# test modules): asserted results are deferred, branched-on results run at once (sigsets.py).
+BLOCK_SRC = """
+def process_attestation(shim, pks, m, sig):             # specs/phase0/beacon-chain.md:2005 (via :790)
+    assert is_valid_indexed_attestation(shim, pks, m, sig)
+
+
+def is_valid_indexed_attestation(shim, pks, m, sig):    # :776-790
+    return shim.FastAggregateVerify(pks, m, sig)
+
+
+def process_randao(shim, pk, m, sig):                   # :1893
+    assert shim.Verify(pk, m, sig)
+
+
+def process_av(shim, pks, msgs, sig):
+    assert shim.AggregateVerify(pks, msgs, sig)
+
+
+def process_sync_aggregate(shim, pks, m, sig):          # specs/altair/beacon-chain.md:608
+    assert shim.eth_fast_aggregate_verify(pks, m, sig)
+
+
+def apply_deposit(shim, pk, m, sig, registry):          # specs/phase0/beacon-chain.md:2055
+    if shim.Verify(pk, m, sig):
+        registry.append(pk)
+"""
+
+
+def _block_fns():
+    ns = {}
+    exec(compile(BLOCK_SRC, "<generated spec>", "exec"), ns)
+    return ns
+
+
 def test_signature_sets_block(b):
     """One block's worth of calls through the shim under sigsets.deferred(): resident FAV and Verify go to
-    the indexed batch, raw-key Verify and AggregateVerify to the AV batch, non-resident FAV per call."""
+    the indexed batch, raw-key Verify and AggregateVerify to the AV batch, non-resident FAV per call.  A deposit
+    with an invalid proof of possession (apply_deposit branches on Verify) is verified at once and skipped, and
+    the block stays valid (test_process_deposit.py:255-287)."""
     from bls_mi355x import bls as shim
     from bls_mi355x import sigsets
 
+    f = _block_fns()
     shim.use_mi355x()
     shim.bls_active = True
     reg = b.Registry()
@@ -143,25 +181,34 @@ def test_signature_sets_block(b):
     fav_sigs = [OC.Sign(sum(sks[k] for k in c) % O.R, m[j]) for j, c in enumerate(committees)]
     outsider = _keys(b, [1000, 1001])
     expect = []
+    deposits = []
     with sigsets.deferred(reg, check=False) as col:
         for j, c in enumerate(committees):  # attestations (resident keys)
             expect.append(j != 1)
             sig = fav_sigs[j] if j != 1 else fav_sigs[0]
-            assert shim.FastAggregateVerify([pks[k] for k in c], m[j], sig) is True
-        assert shim.Verify(pks[5], m[3], OC.Sign(6, m[3])) is True; expect.append(True)          # resident
-        assert shim.Verify(outsider[0], b"short", OC.Sign(1000, b"short")) is True; expect.append(True)  # AV route
-        assert shim.AggregateVerify(outsider, [m[4], m[5]],
-                                    shim.Aggregate([OC.Sign(1000, m[4]), OC.Sign(1001, m[5])])) is True
+            f["process_attestation"](shim, [pks[k] for k in c], m[j], sig)
+        f["process_randao"](shim, pks[5], m[3], OC.Sign(6, m[3])); expect.append(True)            # resident
+        f["process_randao"](shim, outsider[0], b"short", OC.Sign(1000, b"short")); expect.append(True)  # AV route
+        f["process_av"](shim, outsider, [m[4], m[5]], shim.Aggregate([OC.Sign(1000, m[4]), OC.Sign(1001, m[5])]))
         expect.append(True)
-        assert shim.FastAggregateVerify(outsider, m[6], OC.Sign(2001, m[6])) is True; expect.append(True)  # single
-        assert shim.FastAggregateVerify([pks[0]], m[7], b"\x00" * 10) is True; expect.append(False)
-        assert shim.eth_fast_aggregate_verify([], m[7], G2_INF) is True  # eth special case, not recorded
-    assert col.results == expect
+        f["process_attestation"](shim, outsider, m[6], OC.Sign(2001, m[6])); expect.append(True)  # single
+        f["process_attestation"](shim, [pks[0]], m[7], b"\x00" * 10); expect.append(False)       # malformed
+        f["process_sync_aggregate"](shim, [], m[7], G2_INF)  # eth special case, not recorded
+        # deposits: the proof of possession is branched on, so these run at once with their real verdicts
+        f["apply_deposit"](shim, outsider[1], m[2], OC.Sign(1000, m[2]), deposits)  # signed by another key
+        f["apply_deposit"](shim, outsider[1], m[2], OC.Sign(1001, m[2]), deposits)  # valid PoP
+    assert col.results == expect and col.eager == 2 and deposits == [outsider[1]]
     indexed, av, single = col.plan()
-    assert [i for i, _ in indexed] == [0, 1, 2, 3] and av == [4, 5] and single == [6, 7]
+    assert [i for i, _ in indexed] == [0, 1, 2, 3] and av == [4, 5] and single == [6]  # 7 is malformed
+    # a block with only valid signatures and an invalid-PoP deposit: no AssertionError at exit
+    deposits.clear()
+    with sigsets.deferred(reg) as col2:
+        f["process_attestation"](shim, [pks[k] for k in committees[0]], m[0], fav_sigs[0])
+        f["apply_deposit"](shim, outsider[0], m[2], OC.Sign(1001, m[2]), deposits)
+    assert col2.results == [True] and deposits == []
     with pytest.raises(AssertionError):
         with sigsets.deferred(reg):
-            shim.FastAggregateVerify([pks[k] for k in committees[1]], m[1], fav_sigs[0])
+            f["process_attestation"](shim, [pks[k] for k in committees[1]], m[1], fav_sigs[0])
     # outside the block the shim verifies immediately again
     assert shim.FastAggregateVerify([pks[k] for k in committees[1]], m[1], fav_sigs[0]) is False
 

@@ -68,4 +68,60 @@ def test_reference_backend_switches_raise_without_wheels():
         with pytest.raises(ImportError):
             fn()
     bls.use_fastest()
-    assert bls.bls is bls.mi355x_bls
+    assert bls.bls is bls.fastest_bls
+
+
+def test_fastest_bls_contract():
+    """E/utils/bls.py:57-76: the default backend is fastest_bls; its signature attributes are the MI355X
+    backend's (milagro's role) and its curve classes are the MI355X curve objects (arkworks' role), so every
+    `bls == arkworks_bls or bls == fastest_bls` helper branch of the reference (:225, :244, ... :390) holds."""
+    from bls_mi355x import bls, curve
+    from bls_mi355x.backend import mi355x_bls
+
+    bls.use_mi355x()
+    assert bls.bls == bls.fastest_bls and bls.Scalar is curve.Scalar
+    for name in ("Sign", "Verify", "Aggregate", "AggregateVerify", "FastAggregateVerify", "SkToPk", "_AggregatePKs"):
+        assert getattr(bls.fastest_bls, name) is getattr(mi355x_bls, name), name
+    assert (bls.fastest_bls.G1, bls.fastest_bls.G2, bls.fastest_bls.GT) == (curve.G1Point, curve.G2Point, curve.GT)
+
+
+def test_helpers_take_the_fastest_branch(monkeypatch):
+    """add / neg / multiply / multi_exp / pairing_check / Z1 / G1 dispatch to the curve objects (no device call:
+    the point operations are replaced by recorders)."""
+    from bls_mi355x import bls, curve
+
+    bls.use_mi355x()
+    seen = []
+    monkeypatch.setattr(curve._Point, "__add__", lambda a, b: seen.append("add") or a)
+    monkeypatch.setattr(curve._Point, "__neg__", lambda a: seen.append("neg") or a)
+    monkeypatch.setattr(curve._Point, "__mul__", lambda a, k: seen.append(("mul", type(k).__name__, int(k))) or a)
+    monkeypatch.setattr(curve.G1Point, "multiexp_unchecked",
+                        classmethod(lambda cls, p, k: seen.append(("msm", len(p), type(k[0]).__name__)) or p[0]))
+    monkeypatch.setattr(curve.GT, "multi_pairing", classmethod(lambda cls, a, b: seen.append(("pair", len(a))) or cls.one()))
+    g = bls.G1()
+    assert g.to_compressed_bytes() == curve.G1_GENERATOR and bls.Z1().to_compressed_bytes() == curve.G1_IDENTITY
+    assert bls.G1_to_bytes48(bls.add(g, bls.neg(g))) == curve.G1_GENERATOR
+    bls.multiply(g, 5)
+    bls.multiply(g, curve.Scalar(-1))
+    bls.multi_exp([g, g], [1, 2])
+    assert bls.pairing_check([[g, bls.G2()], [g, bls.neg(bls.G2())]]) is True
+    assert seen == ["neg", "add", ("mul", "Scalar", 5), ("mul", "Scalar", curve.R - 1), ("msm", 2, "Scalar"), "neg",
+                    ("pair", 2)]
+    with pytest.raises(Exception, match="zero points"):
+        bls.multi_exp([], [])
+
+
+def test_scalar_field_arithmetic():
+    from bls_mi355x.curve import R, Scalar
+
+    class BLSFieldElement(Scalar):  # pysetup/spec_builders/deneb.py:17-18
+        pass
+
+    a, b = BLSFieldElement(7), BLSFieldElement(R + 3)
+    assert int(b) == 3 and isinstance(a + b, BLSFieldElement)
+    assert int(a - b) == 4 and int(b - a) == R - 4 and int(-a) == R - 7
+    assert int(a * b) == 21 and int(a / b) == 7 * pow(3, -1, R) % R
+    assert a.pow(BLSFieldElement(3)) == BLSFieldElement(343) and int(a.inverse() * a) == 1
+    assert a == 7 and a != b and hash(a) == hash(Scalar(7))
+    with pytest.raises(ZeroDivisionError):
+        BLSFieldElement(0).inverse()

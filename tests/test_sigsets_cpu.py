@@ -60,6 +60,47 @@ def test_routing(fakes):
     assert av == [3, 4, 5, 6] and single == [8]
 
 
+# Spec-shaped call sites, compiled from source like the generated spec modules (pytest rewrites the asserts
+# of test modules, so these must not be defined in this file's own code).
+SPEC_SRC = """
+def _process_randao(shim, pk, m, sig):  # specs/phase0/beacon-chain.md:1893
+    assert shim.Verify(pk, m, sig)
+
+
+def _is_valid_indexed_attestation(shim, pks, m, sig):  # :776-790
+    return shim.FastAggregateVerify(pks, m, sig)
+
+
+def _process_attestation(shim, pks, m, sig):  # :2005
+    assert _is_valid_indexed_attestation(shim, pks, m, sig)
+
+
+def _process_av(shim, pks, msgs, sig):
+    assert shim.AggregateVerify(pks, msgs, sig), "aggregate verify"
+
+
+def _process_sync_aggregate(shim, pks, m, sig):  # specs/altair/beacon-chain.md:608
+    assert shim.eth_fast_aggregate_verify(pks, m, sig)
+
+
+def _apply_deposit(shim, pk, m, sig, applied):  # specs/phase0/beacon-chain.md:2055
+    if shim.Verify(pk, m, sig):
+        applied.append(pk)
+
+
+def _compare(shim, pk, m, sig):
+    return shim.Verify(pk, m, sig) is False
+"""
+_spec = {}
+exec(compile(SPEC_SRC, "<generated spec>", "exec"), _spec)
+_process_randao = _spec["_process_randao"]
+_process_attestation = _spec["_process_attestation"]
+_process_av = _spec["_process_av"]
+_process_sync_aggregate = _spec["_process_sync_aggregate"]
+_apply_deposit = _spec["_apply_deposit"]
+_compare = _spec["_compare"]
+
+
 def test_deferred_records_and_checks(fakes, monkeypatch):
     sigsets, calls = fakes
     from bls_mi355x import bls as shim
@@ -69,18 +110,98 @@ def test_deferred_records_and_checks(fakes, monkeypatch):
     keys = [_pk(i) for i in range(4)]
     shim.bls_active = True
     with sigsets.deferred(FakeRegistry(keys), check=False) as col:
-        assert shim.FastAggregateVerify(keys, b"\x03" * 32, b"\x04" * 96) is True
-        assert shim.Verify(keys[1], b"\x03" * 32, b"\x04" * 96) is True
-        assert shim.AggregateVerify(keys[:1], [b"m"], b"\x04" * 96) is True
-        assert shim.eth_fast_aggregate_verify([], b"\x03" * 32, b"\xc0" + bytes(95)) is True
+        _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
+        _process_randao(shim, keys[1], b"\x03" * 32, b"\x04" * 96)
+        _process_av(shim, keys[:1], [b"m"], b"\x04" * 96)
+        _process_sync_aggregate(shim, [], b"\x03" * 32, b"\xc0" + bytes(95))  # special case: no set
     assert shim._collector is None
-    assert len(col) == 3 and col.results == [True, True, True]
+    assert len(col) == 3 and col.results == [True, True, True] and col.eager == 0
     assert calls["fav"] == ([0, 1, 2, 3, 1], [0, 4, 5], 2, 2)
     assert calls["av"] == [1]
     with pytest.raises(AssertionError, match="set 0"):
         with sigsets.deferred(None):
-            shim.FastAggregateVerify([_pk(50)], b"\x03" * 32, b"\x04" * 96)  # per-call path -> False
+            _process_attestation(shim, [_pk(50)], b"\x03" * 32, b"\x04" * 96)  # per-call path -> False
     assert shim._collector is None
+
+
+def test_deferred_branching_site_gets_the_real_verdict(fakes, monkeypatch):
+    """apply_deposit branches on Verify: an invalid proof of possession skips the deposit and the block stays
+    valid (test_process_deposit.py:255-287), so inside deferred() that call runs at once."""
+    sigsets, _ = fakes
+    from bls_mi355x import bls as shim
+    from bls_mi355x.backend import mi355x_bls
+
+    seen = []
+    monkeypatch.setattr(mi355x_bls, "Verify", staticmethod(lambda pk, m, s: seen.append(pk) or pk == _pk(1)))
+    monkeypatch.setattr(shim.fastest_bls, "Verify", mi355x_bls.Verify)
+    applied = []
+    with sigsets.deferred(FakeRegistry([_pk(1)])) as col:  # no AssertionError at exit
+        _apply_deposit(shim, _pk(2), b"\x05" * 32, b"\x06" * 96, applied)  # invalid PoP: skipped
+        _apply_deposit(shim, _pk(1), b"\x05" * 32, b"\x06" * 96, applied)  # valid: applied
+        assert _compare(shim, _pk(2), b"\x05" * 32, b"\x06" * 96)  # a comparison is not an assert
+    assert applied == [_pk(1)] and seen == [_pk(2), _pk(1), _pk(2)]
+    assert len(col) == 0 and col.eager == 3 and col.results == []
+
+
+PATTERNS_SRC = """
+import sys
+from bls_mi355x.sigsets import result_is_asserted
+
+
+def probe():
+    return result_is_asserted(sys._getframe(1))
+
+
+def asserted():
+    assert probe()
+
+
+def asserted_msg():
+    assert probe(), "message"
+
+
+def returned():
+    return probe()
+
+
+def through_return():
+    assert returned()
+
+
+def negated():
+    assert not probe()
+
+
+def branched():
+    if probe():
+        return True
+    return False
+
+
+def stored():
+    x = probe()
+    return x
+"""
+
+
+def test_result_is_asserted_bytecode_patterns():
+    ns = {}
+    exec(compile(PATTERNS_SRC, "<patterns>", "exec"), ns)
+    ns["asserted"]()
+    ns["asserted_msg"]()
+    ns["through_return"]()
+    ns["negated"]()  # `assert not f()`: f must see False (deferring would return True and fail the assert)
+    assert ns["branched"]() is False and ns["stored"]() is False and ns["returned"]() is False
+
+
+def test_wrong_lengths_are_false_not_errors(fakes):
+    sigsets, calls = fakes
+    s = sigsets.SignatureSets(FakeRegistry([_pk(0)]))
+    s.add_verify(b"\x01" * 47, b"\x02" * 32, b"\x03" * 96)          # short key
+    s.add_aggregate_verify([b"\x01" * 49], [b"m"], b"\x03" * 96)     # long key
+    s.add_fast_aggregate_verify([_pk(0)], b"\x02" * 32, b"\x03" * 95)  # short signature
+    assert all(x.malformed for x in s.sets)
+    assert s.verify() == [False, False, False]
 
 
 def test_deferred_restores_on_exception(fakes):

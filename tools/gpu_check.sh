@@ -12,24 +12,30 @@ export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
       tail -3 "$OUT/pytest.log" ;;
     bench)
       timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
         || { tail -30 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
+    configs)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py -x -v --timeout 600 --timeout-method thread \
+        > "$OUT/configs.log" 2>&1 || { tail -40 "$OUT/configs.log"; exit 1; }
+      tail -3 "$OUT/configs.log" ;;
     benchq)
       timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu > "$OUT/bench.json" 2> "$OUT/bench.err" \
         || { tail -30 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
     prof)
       (cd /tmp && true)
+      # the bench command itself (the CPU leg is host-only and skipped under the profiler)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
-        python3 bench.py --steps 3 --warmup 1 --no-cpu > "$OUT/prof.log" 2>&1 \
+        python3 bench.py --no-cpu > "$OUT/prof.log" 2>&1 \
         || { tail -30 "$OUT/prof.log"; exit 1; }
       db=$(find "$OUT/prof" -name '*.db' | head -n 1)
-      if [ -n "$db" ]; then python3 tools/rocprof_summary.py "$db" "$OUT/kernel_stats.md" > /dev/null; fi
+      if [ -n "$db" ]; then python3 tools/rocprof_summary.py "$db" "$OUT/kernel_stats.md" "$OUT/rocprof_kernel_avg.json" \
+        "profiles/${TAG}_kernel_stats.md (rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu)" > /dev/null; fi
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
       tail -2 "$OUT/prof.log" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace --stats database (rocpd SQLite) into a
-per-kernel table (calls, total/avg/min/max duration, VGPRs, scratch)."""
+per-kernel table (calls, total/avg/min/max duration, VGPRs, scratch), and
+optionally a JSON of per-kernel average durations (bench.py reads the
+committed copy, profiles/rocprof_kernel_avg.json, to set its live hipEvent
+roofline figure beside the rocprof one)."""
+import json
 import sqlite3
 import sys
 
 
-def main(db, out=None):
+def main(db, out=None, out_json=None, source=None):
     c = sqlite3.connect(db)
     rows = c.execute(
         "select name, count(*), sum(duration), avg(duration), min(duration), max(duration), "
@@ -22,8 +26,13 @@ def main(db, out=None):
     text = "\n".join(lines) + "\n"
     if out:
         open(out, "w").write(text)
+    if out_json:
+        avg = {r[0].split("(")[0].replace("void ", "").replace("bls::", ""): round(r[3] / 1e6, 4) for r in rows}
+        with open(out_json, "w") as fh:
+            json.dump({"source": source or out or db, "avg_ms": avg}, fh, indent=1, sort_keys=True)
     print(text)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    a = sys.argv[1:]
+    main(a[0], a[1] if len(a) > 1 else None, a[2] if len(a) > 2 else None, a[3] if len(a) > 3 else None)
