@@ -50,10 +50,12 @@ FME_OPS = 288  # one 381-bit Montgomery multiplication = 288 v_mad_u64_u32 (SURV
 SHA_OPS = 2400  # one SHA-256 compression
 MEASURED_MAD_OPS = 31.3e12  # sustained v_mad_u64_u32 lane-ops/s, profiles/r01_s2_madrate_microbench.txt
 SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
-LANE_KERNELS = ("miller", "miller_lines", "sig_vm")  # one lane per item, full register file (bls_miller_lane.hip, bls_chain_lane.hip)
+# lanes per item of the lane kernels (full register file, one wave per SIMD): k_miller_acc2 two lanes per pair
+# (bls_miller_pair.hip), k_miller_lines and k_sig_lane one (bls_miller_lane.hip, bls_chain_lane.hip)
+LANE_KERNELS = {"miller": 2, "miller_lines": 1, "sig_vm": 1}
 GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
 # profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
-KERNEL_SYMBOL = {"miller": "k_miller_acc", "miller_lines": "k_miller_lines", "fav_gather": "k_fav_gather<16>"}
+KERNEL_SYMBOL = {"miller": "k_miller_acc2", "miller_lines": "k_miller_lines", "fav_gather": "k_fav_gather<16>"}
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 
 
@@ -321,8 +323,8 @@ def main():
             pass
     if roof is not None:
         roof["frac_of_measured_mad_rate"] = round(roof["achieved"] * 1e12 / MEASURED_MAD_OPS, 5)
-        if dom in LANE_KERNELS:  # one lane per item: the launch occupies ceil(B/64) of the 1024 SIMDs
-            occ = min(1.0, ((B + 63) // 64) / (cus * 4))
+        if dom in LANE_KERNELS:  # k lanes per item, one wave per SIMD: the launch holds ceil(k B / 64) SIMDs
+            occ = min(1.0, ((LANE_KERNELS[dom] * B + 63) // 64) / (cus * 4))
             roof["occupied_simd_frac"] = round(occ, 4)
             roof["frac_of_occupied_simds"] = round(roof["frac"] / occ, 4)
     # secondary figure: algorithmic HBM bytes of the registry gather per launch / its duration

@@ -235,18 +235,22 @@ def pairing_check(pairs, ctx=None) -> bool:
     return c.check(c.lib.bls_pairing_check(c.h, b"".join(g1), b"".join(g2), len(g1))) == 1
 
 
-def g1_multi_exp(points48, scalars, ctx=None) -> bytes:
-    """KZG multi_exp / g1_lincomb: compressed sum [k_i] P_i; scalars are ints (0 <= k < 2^256)."""
+def g1_multi_exp(points48, scalars, ctx=None, subgroup_check: bool = False) -> bytes:
+    """KZG multi_exp / g1_lincomb on compressed points: sum [k_i] P_i (E/utils/bls.py:262-296 -> arkworks
+    G1.multiexp_unchecked, i.e. no subgroup check unless asked); scalars are ints (0 <= k < 2^256).  Raises on
+    an empty input (E/utils/bls.py:270-271) and on an invalid encoding, like the reference."""
     c = ctx or _native.context()
     pts = [bytes(p) for p in points48]
     ks = [int(k) for k in scalars]
+    if not pts or not ks:
+        raise ValueError("Cannot call multi_exp with zero points or zero scalars")
     if len(pts) != len(ks):
         raise ValueError("one scalar per point")
     if any(len(p) != 48 for p in pts) or any(not 0 <= k < 1 << 256 for k in ks):
         raise ValueError("need 48-byte points and 256-bit scalars")
     out = ctypes.create_string_buffer(48)
-    rc = c.check(c.lib.bls_g1_multi_exp(c.h, b"".join(pts), b"".join(k.to_bytes(32, "big") for k in ks), len(pts),
-                                        out))
+    rc = c.check(c.lib.bls_multi_exp(c.h, 1, b"".join(pts), b"".join(k.to_bytes(32, "big") for k in ks), len(pts),
+                                     1 if subgroup_check else 0, out))
     if rc != 1:
         raise ValueError("invalid G1 point encoding")
     return out.raw

@@ -54,6 +54,7 @@ struct Job {
   hipStream_t stream3 = nullptr;  // concurrent branch: sum r_i sigma_i (MSM) + its Miller loop
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sig = nullptr, ev_msm = nullptr, ev_gather = nullptr;
   hipEvent_t ev_partial = nullptr;  // the batch's 576-byte partial is in h_partial
+  hipEvent_t ev_h2c = nullptr, ev_fb = nullptr, ev_fe = nullptr;  // hand-offs to the context-wide aux streams
   uint8_t* h_partial = nullptr;     // pinned host copy of the partial
   Buf buf[NSLOT];
   // last prepared FAV batch
@@ -71,6 +72,12 @@ struct bls_ctx {
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
   std::string err;
+  // Context-wide streams for the kernels with large private segments (the h2c
+  // fallback, 6,000 B/lane; final-exponentiation checks, 3,296 B/lane): the
+  // runtime gives every hardware queue that runs such a kernel a scratch
+  // reservation of (private segment x device wave slots), so they run on two
+  // queues instead of on every job's (see k_h2c_fallback).
+  hipStream_t fb_stream = nullptr, fe_stream = nullptr;
   // registry (HBM resident): 96-B RegKey records, validity in x's top bit
   RegKey* reg = nullptr;
   size_t reg_n = 0;
@@ -222,13 +229,48 @@ void prof_collect(bls_ctx* c) {
     LK(expr);                   \
   } while (0)
 
+// Final-exponentiation check of the product of f[0 .. n) on the context's FE
+// stream, after the current job's stream: 1 / 0.
 int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
   int* d_r;
   SCR(S_INT, 4, d_r);
-  PROF(7, launch_final_check_wave(ctx->j->stream, f, n, d_r));
+  Job& J = *ctx->j;
+  HIPCK(hipEventRecord(J.ev_fe, J.stream));
+  HIPCK(hipStreamWaitEvent(ctx->fe_stream, J.ev_fe, 0));
+  PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
   int r = 0;
-  CK(d2h(ctx, &r, d_r, sizeof r));
+  HIPCK(hipMemcpyAsync(&r, d_r, sizeof r, hipMemcpyDeviceToHost, ctx->fe_stream));
+  HIPCK(hipStreamSynchronize(ctx->fe_stream));
   return r ? 1 : 0;
+}
+
+// nsel independent checks res[k] = (FE(f[sel[k]]) == 1) on the FE stream, after
+// the job's stream (bisection rounds, AggregateVerify per-item checks).
+int run_final_checks_sel(bls_ctx* ctx, const Fp12* f, const uint32_t* sel, size_t nsel, uint32_t* d_sel, int* d_res,
+                         int* res) {
+  if (!nsel) return 0;
+  Job& J = *ctx->j;
+  hipStream_t fe = ctx->fe_stream;
+  HIPCK(hipEventRecord(J.ev_fe, J.stream));
+  HIPCK(hipStreamWaitEvent(fe, J.ev_fe, 0));
+  HIPCK(hipMemcpyAsync(d_sel, sel, 4 * nsel, hipMemcpyHostToDevice, fe));
+  PROF2(8, fe, launch_final_check_sel(fe, f, d_sel, nsel, d_res));
+  HIPCK(hipMemcpyAsync(res, d_res, 4 * nsel, hipMemcpyDeviceToHost, fe));
+  HIPCK(hipStreamSynchronize(fe));
+  return 0;
+}
+
+// hash_to_G2 exceptional items (k_h2c_fallback) on the context's fallback
+// stream, between the h2c phases on `st` and whatever `st` runs next.
+int h2c_fallback(bls_ctx* ctx, hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, const int* flag,
+                 G2A* H) {
+  Job& J = *ctx->j;
+  HIPCK(hipEventRecord(J.ev_h2c, st));
+  HIPCK(hipStreamWaitEvent(ctx->fb_stream, J.ev_h2c, 0));
+  LK(launch_h2c_fallback(ctx->fb_stream, B, msgs, offs, flag, H));
+  HIPCK(hipEventRecord(J.ev_fb, ctx->fb_stream));
+  HIPCK(hipStreamWaitEvent(st, J.ev_fb, 0));
+  return 0;
 }
 
 __global__ void k_set_neg_g1(G1A* p) {
@@ -274,6 +316,9 @@ static bool job_init(Job& J, int prio_hi) {
          hipEventCreateWithFlags(&J.ev_msm, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_gather, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_partial, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_h2c, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_fb, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_fe, hipEventDisableTiming) == hipSuccess &&
          hipHostMalloc((void**)&J.h_partial, 576, hipHostMallocDefault) == hipSuccess;
 }
 
@@ -283,7 +328,7 @@ static void job_destroy(Job& J) {
     if (s) (void)hipStreamSynchronize(s);
   for (auto& b : J.buf)
     if (b.p) (void)hipFree(b.p);
-  hipEvent_t es[6] = {J.ev_fork, J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial};
+  hipEvent_t es[9] = {J.ev_fork, J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial, J.ev_h2c, J.ev_fb, J.ev_fe};
   for (hipEvent_t e : es)
     if (e) (void)hipEventDestroy(e);
   if (J.h_partial) (void)hipHostFree(J.h_partial);
@@ -311,6 +356,11 @@ int bls_ctx_create(int device, bls_ctx** out) {
       return BLS_E_DEVICE;
     }
   }
+  if (hipStreamCreateWithFlags(&c->fb_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->fe_stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+    bls_ctx_destroy(c);
+    return BLS_E_DEVICE;
+  }
   *out = c;
   return 0;
 }
@@ -320,6 +370,11 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (Job& J : ctx->jobs) job_destroy(J);
+  for (hipStream_t s : {ctx->fb_stream, ctx->fe_stream})
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
   for (auto& p : ctx->prof_pending) ctx->prof_pool.push_back(p.second);
   for (auto& p : ctx->prof_pool) {
     (void)hipEventDestroy(p.first);
@@ -390,6 +445,7 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
   LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, U, hf, Q, flag));
+  CK(h2c_fallback(ctx, st2, 1, d_msg, d_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
   HIPCK(hipEventRecord(J.ev_sig, st3));
@@ -399,12 +455,12 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
   LK(launch_miller2(st, P, Q, nullptr, 2, f));  // rejected inputs are identities here; `live` decides
-  PROF(7, launch_final_check_wave(st, f, 1, d_r));
-  int r[2] = {0, 0};
-  HIPCK(hipMemcpyAsync(&r[0], ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-  HIPCK(hipMemcpyAsync(&r[1], d_r, sizeof(int), hipMemcpyDeviceToHost, st));
-  HIPCK(hipStreamSynchronize(st));
-  return (r[0] && r[1]) ? 1 : 0;
+  int live = 0;
+  HIPCK(hipMemcpyAsync(&live, ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+  const int fe = run_final_check(ctx, f);  // orders after st
+  if (fe < 0) return fe;
+  HIPCK(hipStreamSynchronize(st));  // `live` is pageable host memory
+  return (live && fe) ? 1 : 0;
 }
 
 static bool percall_lane() {  // A/B knob: the previous one-lane kernels
@@ -499,6 +555,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
     SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
     SCR(S_AV_FLAG, n, d_flag);
     LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_u, d_hf, Q, d_flag));
+    CK(h2c_fallback(ctx, ctx->j->stream, n, d_msgs, d_offs, d_flag, Q));
   }
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->j->stream, P + n);
   LK(hipGetLastError());
@@ -797,9 +854,11 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_RPJ, B, rpj);
   // Miller loop of (r_i apk_i, H_i): split (G2 lines on stream2 right after
   // hash_to_G2, f accumulation on stream1) unless BLS_ML_MODE=fused / st1
+  // 3 (default): lines on stream2, f accumulated by k_miller_acc2 (two lanes per pair);
+  // A/B knobs: BLS_ML_MODE=acc1 (k_miller_acc, one lane per pair), st1 (both on stream1), fused (k_miller_lane)
   static const int ml_mode = [] {
     const char* m = getenv("BLS_ML_MODE");
-    return !m ? 2 : !strcmp(m, "fused") ? 0 : !strcmp(m, "st1") ? 1 : 2;
+    return !m ? 3 : !strcmp(m, "fused") ? 0 : !strcmp(m, "st1") ? 1 : !strcmp(m, "acc1") ? 2 : 3;
   }();
   uint32_t* mlines = nullptr;
   if (ml_mode) SCR(S_MLINES, miller_lines_u32(B), mlines);
@@ -822,7 +881,8 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   HIPCK(hipStreamWaitEvent(st2, ctx->j->ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, hcf, H, flag));
-  if (ml_mode == 2) PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
+  CK(h2c_fallback(ctx, st2, B, d_msgs, nullptr, flag, H));
+  if (ml_mode >= 2) PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
   HIPCK(hipEventRecord(ctx->j->ev_join, st2));
   PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
   HIPCK(hipEventRecord(ctx->j->ev_sig, st3));
@@ -853,7 +913,9 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
   } else {
     if (ml_mode == 1) PROF(12, launch_miller_lines(st, H, B, mlines));
-    if (ml_mode)
+    if (ml_mode == 3)
+      PROF(5, launch_miller_acc2(st, rP, H, status, B, mlines, f));
+    else if (ml_mode)
       PROF(5, launch_miller_acc(st, rP, H, status, B, mlines, f));
     else
       PROF(5, launch_miller_lane(st, rP, H, status, B, f));
@@ -925,10 +987,8 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
     const size_t n = cand.size();
     sel.resize(n);
     for (size_t k = 0; k < n; k++) sel[k] = (uint32_t)(off[L] + cand[k]);
-    CK(h2d(ctx, d_sel, sel.data(), 4 * n));
-    PROF(8, launch_final_check_sel(st, tree, d_sel, n, d_res));
     res.resize(n);
-    CK(d2h(ctx, res.data(), d_res, 4 * n));
+    CK(run_final_checks_sel(ctx, tree, sel.data(), n, d_sel, d_res, res.data()));
     ctx->j->bis_checks += n;
     ctx->j->bis_rounds += 1;
     std::vector<uint32_t> next;
@@ -1105,6 +1165,7 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
     SCR(S_AV_HCF, h2c_scratch_fd(total), d_hf);
     SCR(S_AV_FLAG, total, d_flag);
     LK(launch_h2c_msgs(st, total, d_msgs, d_moffs, d_u, d_hf, d_h, d_flag));
+    CK(h2c_fallback(ctx, st, total, d_msgs, d_moffs, d_flag, d_h));
   }
   LK(launch_av_items(st, B, d_io, d_pok, d_sok, d_sa, d_rsc, d_status, P2, Q2));
   LK(launch_av_pairs(st, total, d_pitem, d_status, d_rsc, d_pa, d_h, P2, Q2));
@@ -1122,11 +1183,9 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
     SCR(S_AV_SEL, sel.size(), d_sel);
     SCR(S_AV_FI, B, fi);
     SCR(S_AV_RES, sel.size(), d_res);
-    CK(h2d(ctx, d_sel, sel.data(), sel.size() * sizeof(uint32_t)));
     LK(launch_fp12_seg_prod(st, f, d_io, B, fi));
-    LK(launch_final_check_sel(st, fi, d_sel, sel.size(), d_res));
     std::vector<int> res(sel.size());
-    CK(d2h(ctx, res.data(), d_res, sel.size() * sizeof(int)));
+    CK(run_final_checks_sel(ctx, fi, sel.data(), sel.size(), d_sel, d_res, res.data()));
     for (size_t k = 0; k < sel.size(); k++) status[sel[k]] = res[k];
     ctx->j->bis_checks = sel.size();
     ctx->j->bis_rounds = 1;

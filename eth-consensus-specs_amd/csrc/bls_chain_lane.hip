@@ -78,30 +78,44 @@ BLS_HD PP<F> pp_add_aff(const PP<F>& p, const F& x2, const F& y2) {
   return pp_finish(t0, t1, ln_b3(p.z), t3, t4, y3);
 }
 
+// Two independent chains per item, run by DIFFERENT waves (a wave-uniform
+// branch on blockIdx, so no lane diverges): blocks [0, nb) walk r_i apk_i in
+// G1, blocks [nb, 2 nb) walk [|x|] sigma_i in G2 and write the verdict.  Each
+// wave holds one chain's state instead of both, which keeps the G2 chain's
+// wave free of spills, and the launch is twice the waves.
 // gstat: the gather's per-item status (read-only here: the MSM on another
 // stream reads it concurrently); status: this kernel's verdict.
 __global__ void __launch_bounds__(64) k_sig_lane(size_t B, const int* gstat, int* status, const int* dstat,
                                                  const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
-  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const unsigned nb = (unsigned)((B + 63) / 64);
+  const bool g2 = blockIdx.x >= nb;
+  const size_t i = (size_t)(g2 ? blockIdx.x - nb : blockIdx.x) * 64 + threadIdx.x;
   if (i >= B) return;
   const bool live = gstat[i] && dstat[i];
+  if (!g2) {  // r * apk: double-and-add from bit 63 (R = identity (0 : 1 : 0) before)
+    if (!live) return;
+    const G1P a = apk[i];
+    const PP<Fp> A{a.x, a.y, a.z};
+    const uint64_t r = rsc[i];
+    PP<Fp> R{fp_zero(), FP_ONE, fp_zero()};
+    if ((r >> 63) & 1ull) R = A;
+#pragma unroll 1
+    for (int b = 62; b >= 0; --b) {
+      R = pp_dbl(R);
+      if ((r >> b) & 1ull) R = pp_add(R, A);
+    }
+    rPj[i] = G1P{R.x, R.y, R.z};
+    return;
+  }
   if (!live) {
     status[i] = 0;
     return;
   }
-  const G2A s = sig[i];
-  const G1P a = apk[i];
-  const PP<Fp> A{a.x, a.y, a.z};
-  const uint64_t r = rsc[i];
-  // r * apk: double-and-add from bit 63 (R = identity (0 : 1 : 0) before)
-  PP<Fp> R{fp_zero(), FP_ONE, fp_zero()};
   // [|x|] sigma: the leading bit of |x| is bit 63
+  const G2A s = sig[i];
   PP<Fp2> M{s.x, s.y, fp2_one()};
-  if ((r >> 63) & 1ull) R = A;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
-    R = pp_dbl(R);
-    if ((r >> b) & 1ull) R = pp_add(R, A);
     M = pp_dbl(M);
     if ((X_ABS >> b) & 1ull) M = pp_add_aff(M, s.x, s.y);
   }
@@ -110,7 +124,6 @@ __global__ void __launch_bounds__(64) k_sig_lane(size_t B, const int* gstat, int
   const Fp2 dx = fp2_sub(f2mul(px, M.z), M.x);
   const Fp2 dy = fp2_add(f2mul(py, M.z), M.y);
   const bool ok = fp2_is_zero(dx) && fp2_is_zero(dy) && !fp2_is_zero(M.z);
-  rPj[i] = G1P{R.x, R.y, R.z};
   status[i] = ok ? 1 : 0;
 }
 
@@ -141,8 +154,8 @@ __global__ void __launch_bounds__(64) k_g2x_lane(size_t B, Fd* hf, int src, int 
 hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
                            const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_lane, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat, apk, sig,
-                     rsc, rPj);
+  hipLaunchKernelGGL(k_sig_lane, dim3(2 * (unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat, apk,
+                     sig, rsc, rPj);
   return hipGetLastError();
 }
 

@@ -193,12 +193,14 @@ __global__ void __launch_bounds__(64) k_h2c_affine(size_t B, const int* status, 
   H[i] = h;
 }
 
-// The fallback runs as ONE 64-lane workgroup striding over the flags: its
-// inlined hash_to_g2 needs ~6 KB of private segment per lane, and the scratch
-// the runtime reserves for a dispatch grows with its grid (a launch over all
-// B items reserved ~60 MB per queue, which with 15+ hardware queues ended in
-// HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Flags are ~never set, so the loop is
-// B / 64 flag loads.
+// The fallback runs as ONE 64-lane workgroup striding over the flags (they
+// are ~never set, so the loop is B / 64 flag loads).  Its hash_to_g2 call
+// chain needs 6,000 B of private segment per lane, and the runtime sizes a
+// hardware queue's scratch by the largest private segment it has run times
+// the device's wave slots -- not by the grid.  Launched on every job's h2c
+// stream, it gave each of those queues that reservation and six jobs in
+// flight exhausted the scratch pool (HSA_STATUS_ERROR_OUT_OF_RESOURCES); the
+// C ABI therefore runs it on one context-wide stream (bls_capi.hip).
 __global__ void __launch_bounds__(64) k_h2c_fallback(size_t B, const uint8_t* msgs32, const int* flag, G2A* H) {
   for (size_t i = threadIdx.x; i < B; i += 64)
     if (flag[i]) H[i] = jac_to_aff(hash_to_g2(msgs32 + 32 * i, 32, DST_POP_FAV, 43));
@@ -359,11 +361,8 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
   if (e != hipSuccess) return e;
   static const int hg = env_g("BLS_H2C_G", 2);  // tuning knobs: items per workgroup
   static const int xg = env_int_or("BLS_XC_G", 5);  // 4/5/6: wave programs (default: shorter h2c latency); 1: lane chains
-  e = hg == 4 ? launch_h2c_phases<4>(st, B, status, U, hf, H, flag, xg)
-              : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_h2c_fallback, dim3(1), dim3(64), 0, st, B, msgs32, flag, H);
-  return hipGetLastError();
+  return hg == 4 ? launch_h2c_phases<4>(st, B, status, U, hf, H, flag, xg)
+                 : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
 }
 
 hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U, Fd* hf,
@@ -372,9 +371,16 @@ hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const 
   hipLaunchKernelGGL(k_h2c_sswu_var, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, env_int_or("BLS_XC_G", 5));
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_h2c_fallback_var, dim3(1), dim3(64), 0, st, B, msgs, offs, flag, H);
+  return launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, env_int_or("BLS_XC_G", 5));
+}
+
+hipError_t launch_h2c_fallback(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, const int* flag,
+                               G2A* H) {
+  if (!B) return hipSuccess;
+  if (offs)
+    hipLaunchKernelGGL(k_h2c_fallback_var, dim3(1), dim3(64), 0, st, B, msgs, offs, flag, H);
+  else
+    hipLaunchKernelGGL(k_h2c_fallback, dim3(1), dim3(64), 0, st, B, msgs, flag, H);
   return hipGetLastError();
 }
 

@@ -52,6 +52,10 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
 // hash_to_G2 (POP DST) of B messages of any length, msgs[offs[i] .. offs[i+1]); same phases as launch_h2c
 hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U, Fd* hf, G2A* H,
                            int* flag);
+// exceptional h2c items (flag set: an isogeny denominator vanished) recomputed by one workgroup; offs == nullptr
+// for 32-byte messages.  Not part of launch_h2c / launch_h2c_msgs: the caller picks its stream (bls_capi.hip).
+hipError_t launch_h2c_fallback(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, const int* flag,
+                               G2A* H);
 hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, const uint8_t* sigs96, const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat);
 // rPj: B projective scratch points (r_i apk_i before the affine conversion)
 hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk_aff,
@@ -67,6 +71,9 @@ size_t miller_lines_u32(size_t n);
 hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L);
 hipError_t launch_miller_acc(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                              Fp12* f);
+// the same f accumulation with two lanes per pair (bls_miller_pair.hip): f.c0 / f.c1 on lanes 2k / 2k+1
+hipError_t launch_miller_acc2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                              Fp12* f);
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
 // nsel independent checks: out[b] = (FE(f[sel[b]]) == 1)
