@@ -18,9 +18,13 @@ struct alignas(16) Fp {
   uint32_t l[12];
 };
 // VM slot form of an Fp value (bls_vm.h): 14 radix-2^29 digits + 2 zero pad
-// words (64 B), canonical residue in Montgomery form.
+// words, canonical residue in Montgomery form, in an 80-B slot.  The VM reads
+// a slot as four ds_read_b128 (d[0..15]); d[16..19] only space the slots.  With
+// 64-B slots, slot s began at bank group (4 s) mod 16 of a ds_read_b128, so
+// the 16 lanes of a group met in 4 groups (rocprofv3: 41-82 % of the VM
+// kernels' LDS cycles were bank conflicts); at 80 B it is (5 s) mod 16.
 struct alignas(16) Fd {
-  uint32_t d[16];
+  uint32_t d[20];
 };
 struct Fp2 {
   Fp c0, c1;  // c0 + c1 * i,  i^2 = -1

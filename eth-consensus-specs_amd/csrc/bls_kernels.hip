@@ -203,21 +203,24 @@ BLS_HD Fp fp_x12(const Fp& a) {  // 3b * a, b = 4
   return fp_add(fp_dbl(a4), a4);
 }
 
+// Inlined products: this is the gather's inner loop (32 mixed additions per lane at
+// n = 512); out-of-line calls cost ~40 % of the mad rate at this occupancy
+// (profiles/r01_s2_fmerate_microbench.txt) and their frames were the kernel's scratch.
 __device__ __forceinline__ G1P g1p_add_aff(const G1P& p, const Fp& x2, const Fp& y2) {
-  Fp t0 = fp_mul_v(p.x, x2);
-  Fp t1 = fp_mul_v(p.y, y2);
-  Fp t3 = fp_sub(fp_sub(fp_mul_v(fp_add(x2, y2), fp_add(p.x, p.y)), t0), t1);
-  const Fp t4 = fp_add(fp_mul_v(y2, p.z), p.y);
-  Fp y3 = fp_add(fp_mul_v(x2, p.z), p.x);
+  Fp t0 = fp_mul_i(p.x, x2);
+  Fp t1 = fp_mul_i(p.y, y2);
+  Fp t3 = fp_sub(fp_sub(fp_mul_i(fp_add(x2, y2), fp_add(p.x, p.y)), t0), t1);
+  const Fp t4 = fp_add(fp_mul_i(y2, p.z), p.y);
+  Fp y3 = fp_add(fp_mul_i(x2, p.z), p.x);
   t0 = fp_add(fp_dbl(t0), t0);
   const Fp t2 = fp_x12(p.z);
   Fp z3 = fp_add(t1, t2);
   t1 = fp_sub(t1, t2);
   y3 = fp_x12(y3);
   G1P r;
-  r.x = fp_sub(fp_mul_v(t3, t1), fp_mul_v(t4, y3));
-  r.y = fp_add(fp_mul_v(t1, z3), fp_mul_v(y3, t0));
-  r.z = fp_add(fp_mul_v(z3, t4), fp_mul_v(t0, t3));
+  r.x = fp_sub(fp_mul_i(t3, t1), fp_mul_i(t4, y3));
+  r.y = fp_add(fp_mul_i(t1, z3), fp_mul_i(y3, t0));
+  r.z = fp_add(fp_mul_i(z3, t4), fp_mul_i(t0, t3));
   return r;
 }
 

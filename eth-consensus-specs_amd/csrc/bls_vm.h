@@ -274,9 +274,15 @@ __device__ __noinline__ void vm_run(const VmProg p, Fd* slots, int item0, int st
         vm_normalise(out.d, a);
         vm_reduce(out.d);
       }
-      out.d[14] = 0;
-      out.d[15] = 0;
-      slots[vm_slot(d & 0x3fffffu, ibase)] = out;
+      {  // the 64 meaningful bytes, as four ds_write_b128 (the slot's last 16 B are padding)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        __attribute__((address_space(3))) u32x4* q =
+            (__attribute__((address_space(3))) u32x4*)(slots + vm_slot(d & 0x3fffffu, ibase));
+        q[0] = u32x4{out.d[0], out.d[1], out.d[2], out.d[3]};
+        q[1] = u32x4{out.d[4], out.d[5], out.d[6], out.d[7]};
+        q[2] = u32x4{out.d[8], out.d[9], out.d[10], out.d[11]};
+        q[3] = u32x4{out.d[12], out.d[13], 0u, 0u};
+      }
     }
     __syncthreads();
   }

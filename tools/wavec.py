@@ -1126,6 +1126,12 @@ INSTANCES = []   # (instance name, program name, frame bases, scratch base)
 
 
 def layout(name, **slots):
+    # Odd item strides: LDS slots are 80 B (Fd, bls_field_types.h), so slot s
+    # starts at bank group (5 s) mod 16 of a ds_read_b128; with an odd stride
+    # the same slot of up to 16 items of one workgroup lands in 16 different
+    # groups (an even stride put items in the same group: 2-16-way conflicts).
+    if "STRIDE" in slots and slots["STRIDE"] % 2 == 0:
+        slots = dict(slots, STRIDE=slots["STRIDE"] + 1)
     LAYOUT[name] = slots
 
 
