@@ -5,6 +5,7 @@
 // big-endian integers (48 bytes per Fp).
 #include "bls_ops.h"
 #include "bls_lane.h"
+#include "bls_tower_inline.h"
 #include <string.h>
 using namespace bls;
 
@@ -26,6 +27,12 @@ static void out_fp12(uint8_t* b, const Fp12& r) {
 }
 
 extern "C" {
+// inline tower of the lane kernels (bls_tower_inline.h): Fp2 product with unreduced operand sums, Fp12 steps
+void hc_f2mul_i(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp2(o, f2mul(in_fp2(a), in_fp2(b))); }
+void hc_f12sqr_i(const uint8_t* a, uint8_t* o) { out_fp12(o, f12sqr(in_fp12(a))); }
+void hc_f12line_i(const uint8_t* f, const uint8_t* l0, const uint8_t* l2, const uint8_t* l3, uint8_t* o) {
+  out_fp12(o, f12line(in_fp12(f), in_fp2(l0), in_fp2(l2), in_fp2(l3)));
+}
 void hc_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp(o, fp_mul(in_fp(a), in_fp(b))); }
 void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp(o, fp_add(in_fp(a), in_fp(b))); }
 void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp(o, fp_sub(in_fp(a), in_fp(b))); }

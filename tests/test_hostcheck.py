@@ -59,6 +59,25 @@ def test_fp2_ops():
     assert ok == 0
 
 
+def test_inline_tower_fp2_product_and_fp12_steps():
+    """f2mul of the inline tower (bls_tower_inline.h), whose Karatsuba sums stay unreduced, and the Fp12 steps
+    built on it, against the oracle -- including the extreme operands (0, 1, p - 1)."""
+    edge = [0, 1, 2, O.P - 1, O.P - 2, (O.P - 1) // 2, 1 << 380]
+    cases = [((x, y), (u, v)) for x in edge for y in edge[:4] for u in edge[:4] for v in edge] + \
+        [(rfp2(), rfp2()) for _ in range(200)]
+    for a, b in cases:
+        a = (a[0] % O.P, a[1] % O.P)
+        b = (b[0] % O.P, b[1] % O.P)
+        assert H.b_fp2(H.call("hc_f2mul_i", H.fp2_b(a), H.fp2_b(b), out=96)) == O.f2_mul(a, b), (a, b)
+    for _ in range(6):
+        a = rfp12()
+        assert H.b_fp12(H.call("hc_f12sqr_i", H.fp12_b(a), out=576)) == O.f12_sqr(a)
+        l0, l2, l3 = rfp2(), rfp2(), rfp2()
+        line = O.f12_from_coeffs([l0, O.F2_ZERO, l2, l3, O.F2_ZERO, O.F2_ZERO])
+        got = H.b_fp12(H.call("hc_f12line_i", H.fp12_b(a), H.fp2_b(l0), H.fp2_b(l2), H.fp2_b(l3), out=576))
+        assert got == O.f12_mul(a, line)
+
+
 def test_fp12_ops():
     for _ in range(4):
         a, b = rfp12(), rfp12()
