@@ -74,6 +74,9 @@ hipError_t launch_miller_acc(hipStream_t st, const G1A* P, const G2A* Q, const i
 // the same f accumulation with two lanes per pair (bls_miller_pair.hip): f.c0 / f.c1 on lanes 2k / 2k+1
 hipError_t launch_miller_acc2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                               Fp12* f);
+// four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values
+hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                              Fp12* f, int G);
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
 // nsel independent checks: out[b] = (FE(f[sel[b]]) == 1)
