@@ -50,12 +50,13 @@ FME_OPS = 288  # one 381-bit Montgomery multiplication = 288 v_mad_u64_u32 (SURV
 SHA_OPS = 2400  # one SHA-256 compression
 MEASURED_MAD_OPS = 31.3e12  # sustained v_mad_u64_u32 lane-ops/s, profiles/r01_s2_madrate_microbench.txt
 SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
-# lanes per item of the lane kernels (full register file, one wave per SIMD): k_miller_acc2 two lanes per pair
-# (bls_miller_pair.hip), k_miller_lines and k_sig_lane one (bls_miller_lane.hip, bls_chain_lane.hip)
-LANE_KERNELS = {"miller": 2, "miller_lines": 1, "sig_vm": 1}
+# lanes per item of the lane kernels (full register file, one wave per SIMD): k_miller_acc4<2> four lanes per two
+# pairs (bls_miller_pair.hip), k_miller_lines2 two per pair (bls_miller_lane.hip), k_sig_lane2 one for the G1
+# chain and two for the G2 chain of an item (bls_chain_lane.hip)
+LANE_KERNELS = {"miller": 2, "miller_lines": 2, "sig_vm": 3}
 GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
 # profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
-KERNEL_SYMBOL = {"miller": "k_miller_acc2", "miller_lines": "k_miller_lines", "fav_gather": "k_fav_gather<16>"}
+KERNEL_SYMBOL = {"miller": "k_miller_acc4<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather<16>"}
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 
 
@@ -67,10 +68,10 @@ def model_fme(n: int):
         "sig_vm": 1200 + 1000 + 400,    # G2 subgroup check, RLC G1, RLC G2 (MSM share)
         "fav_hash": 6600,
         # Miller loop, 4400 FME per pair, split between its two kernels in proportion to the products each
-        # executes: k_miller_acc (f: 62 Fp12 squarings x 36 + 68 sparse line products x 43 = 5156) and
-        # k_miller_lines (T: 63 doublings x 26 + 5 additions x 35 = 1813)
-        "miller": 4400 * 5156 / 6969,
-        "miller_lines": 4400 * 1813 / 6969,
+        # executes per pair: k_miller_acc4<2> (f shared by two pairs: 62 Fp12 squarings x 36 / 2 + 68 sparse
+        # line products x 43 = 4040) and k_miller_lines2 (T: 63 doublings x 26 + 5 additions x 35 = 1813)
+        "miller": 4400 * 4040 / 5853,
+        "miller_lines": 4400 * 1813 / 5853,
     }
 
 

@@ -337,7 +337,7 @@ static hipError_t launch_h2c_phases(hipStream_t st, size_t B, const int* status,
   hipLaunchKernelGGL(k_h2c_iso<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, U, hf, flag);
   for (int pass = 0; pass < 2; pass++) {  // M = [|x|] Q, then M = [|x|] A
     const int src = pass ? HCF_A : HCF_Q;
-    if (xg == 1) {  // default: one lane per item (bls_chain_lane.hip)
+    if (xg == 1) {  // default: lane chains (bls_chain_lane.hip)
       hipError_t e = launch_g2x_lane(st, B, hf, src, HCF_M);
       if (e != hipSuccess) return e;
     } else if (xg == 4)
@@ -360,7 +360,9 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   static const int hg = env_g("BLS_H2C_G", 2);  // tuning knobs: items per workgroup
-  static const int xg = env_int_or("BLS_XC_G", 5);  // 4/5/6: wave programs (default: shorter h2c latency); 1: lane chains
+  // [|x|] chains of cofactor clearing: 1 (default) = two lanes per item (k_g2x_lane2: 1.35-1.37M FAV/s against
+  // 1.33-1.35M for the 5-item wave program); 4/5/6 = wave programs with that many items per workgroup
+  static const int xg = env_int_or("BLS_XC_G", 1);
   return hg == 4 ? launch_h2c_phases<4>(st, B, status, U, hf, H, flag, xg)
                  : launch_h2c_phases<2>(st, B, status, U, hf, H, flag, xg);
 }
@@ -371,7 +373,7 @@ hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const 
   hipLaunchKernelGGL(k_h2c_sswu_var, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, env_int_or("BLS_XC_G", 5));
+  return launch_h2c_phases<2>(st, B, nullptr, U, hf, H, flag, env_int_or("BLS_XC_G", 1));
 }
 
 hipError_t launch_h2c_fallback(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, const int* flag,
