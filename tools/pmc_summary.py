@@ -21,6 +21,22 @@ def main(path, out=None):
         disp[k].add(row["Dispatch_Id"])
         dur[k][row["Dispatch_Id"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
     lds_pass = any("SQ_LDS_IDX_ACTIVE" in acc[k] for k in acc)
+    fetch_pass = any("FETCH_SIZE" in acc[k] for k in acc)
+    if fetch_pass:  # FETCH_SIZE is in KB (MI355X_MICROARCH.md, rocprofv3 section); uncorrected
+        lines = [f"# rocprofv3 --pmc FETCH_SIZE summary of {path} (per dispatch averages, uncorrected)",
+                 "| kernel | disp | ms | FETCH_SIZE KB/dispatch | MB/dispatch | GB/s |",
+                 "|---|---|---|---|---|---|"]
+        for k in sorted(acc, key=lambda k: -sum(dur[k].values())):
+            n = len(disp[k])
+            kb = acc[k].get("FETCH_SIZE", 0) / n
+            ms = sum(dur[k].values()) / n
+            lines.append(f"| {k} | {n} | {ms:.3f} | {kb:.0f} | {kb * 1024 / 1e6:.2f} | "
+                         f"{kb * 1024 / (ms * 1e-3) / 1e9 if ms else 0:.1f} |")
+        text = "\n".join(lines) + "\n"
+        if out:
+            open(out, "w").write(text)
+        print(text)
+        return
     if lds_pass:
         lines = [f"# rocprofv3 --pmc LDS / occupancy summary of {path} (per dispatch averages)",
                  "| kernel | disp | ms | waves | LDS instr/wave | LDS-array cycles | bank-conflict cycles | "
