@@ -9,6 +9,7 @@
 //     complete (exception-free) projective formulas.
 #include "bls_kernels.h"
 #include "bls_lane.h"
+#include "bls_pp_lane.h"
 #include "bls_vm.h"
 
 #include <stdlib.h>
@@ -318,6 +319,145 @@ __global__ void __launch_bounds__(64) k_g1_affine(size_t B, const int* status, c
   rP[i] = o;
 }
 
+// ---------------------------------------------- hash_to_G2 on lane pairs --
+// The phases after SSWU as lane-pair kernels (bls_pp_lane.h pp2_*), fused with
+// their neighbours; they replace the wave-program phases k_h2c_iso / _pre /
+// _post (5,000-wave launches of ~25-60 products per item whose LDS staging
+// and per-level barriers cost more than the arithmetic):
+//   k_h2c_sswu_iso2  lane (item, t): hash_to_field, SSWU of u_t, 3-isogeny of
+//                    its own point (homogeneous projective, tools/wavec.py
+//                    prog_iso_pair), swap, Q = iso(P0) + iso(P1) on the pair
+//   k_g2x_pre2       M = [|x|] Q, then A = psi(Q) - M and
+//                    C = psi^2(2Q) - psi(Q) + M - Q      (prog_clear_pre)
+//   k_g2x_post2      M = [|x|] A, then H = C - M          (prog_clear_post)
+// The formulas are complete (Renes-Costello-Batina), so H is the same point
+// as the wave programs' and its affine form (k_h2c_affine) is bit-identical.
+// Staging is the same hf layout (HCF Fd slots per item).
+namespace {
+
+__device__ __forceinline__ PP<Fp2> pp2_swap(const PP<Fp2>& p) { return PP<Fp2>{cl_swap2(p.x), cl_swap2(p.y), cl_swap2(p.z)}; }
+__device__ __forceinline__ PP<Fp2> pp2_sel(bool c, const PP<Fp2>& a, const PP<Fp2>& b) {
+  return PP<Fp2>{cl_sel(c, a.x, b.x), cl_sel(c, a.y, b.y), cl_sel(c, a.z, b.z)};
+}
+__device__ __forceinline__ PP<Fp2> pp2_neg(const PP<Fp2>& p) { return PP<Fp2>{p.x, fp2_neg(p.y), p.z}; }
+__device__ __forceinline__ PP<Fp2> pp2_psi(const PP<Fp2>& p) {
+  return PP<Fp2>{f2mul(fp2_conj(p.x), PSI_CX), f2mul(fp2_conj(p.y), PSI_CY), fp2_conj(p.z)};
+}
+__device__ __forceinline__ PP<Fp2> pp2_psi2(const PP<Fp2>& p) {
+  return PP<Fp2>{f2mul(p.x, PSI2_CX), f2mul(p.y, PSI2_CY), p.z};
+}
+
+// (x, y) affine on E2' -> iso(x, y) = (xnum yden : y ynum xden : xden yden) on E2 (RFC 9380 App. E.3)
+__device__ __forceinline__ PP<Fp2> iso_proj_lane(const Fp2& x, const Fp2& y) {
+  const Fp2 xx = f2sqr(x), xxx = f2mul(xx, x);
+  const Fp2 xnum = fadd(fadd(f2mul(ISO_XNUM_3, xxx), f2mul(ISO_XNUM_2, xx)), fadd(f2mul(ISO_XNUM_1, x), ISO_XNUM_0));
+  const Fp2 xden = fadd(fadd(xx, f2mul(ISO_XDEN_1, x)), ISO_XDEN_0);
+  const Fp2 ynum = fadd(fadd(f2mul(ISO_YNUM_3, xxx), f2mul(ISO_YNUM_2, xx)), fadd(f2mul(ISO_YNUM_1, x), ISO_YNUM_0));
+  const Fp2 yden = fadd(fadd(xxx, f2mul(ISO_YDEN_2, xx)), fadd(f2mul(ISO_YDEN_1, x), ISO_YDEN_0));
+  return PP<Fp2>{f2mul(xnum, yden), f2mul(f2mul(y, ynum), xden), f2mul(xden, yden)};
+}
+
+// lane 0 writes X, Y.c0; lane 1 Y.c1, Z (six consecutive Fd slots)
+__device__ __forceinline__ void pp2_store(Fd* o, const PP<Fp2>& p, bool hi) {
+  if (!hi) {
+    o[0] = fd_from_fp(p.x.c0);
+    o[1] = fd_from_fp(p.x.c1);
+    o[2] = fd_from_fp(p.y.c0);
+  } else {
+    o[3] = fd_from_fp(p.y.c1);
+    o[4] = fd_from_fp(p.z.c0);
+    o[5] = fd_from_fp(p.z.c1);
+  }
+}
+__device__ __forceinline__ PP<Fp2> pp2_load(const Fd* in) {
+  return PP<Fp2>{Fp2{fp_from_fd(in[0]), fp_from_fd(in[1])}, Fp2{fp_from_fd(in[2]), fp_from_fd(in[3])},
+                 Fp2{fp_from_fd(in[4]), fp_from_fd(in[5])}};
+}
+
+// M = [|x|] Bp (two lanes per item; the leading bit of |x| is bit 63)
+__device__ __forceinline__ PP<Fp2> pp2_mul_xabs(const PP<Fp2>& Bp, bool hi) {
+  PP<Fp2> M = Bp;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    M = pp2_dbl(M, hi);
+    if ((X_ABS >> b) & 1ull) M = pp2_add(M, Bp, hi);
+  }
+  return M;
+}
+
+}  // namespace
+
+// msgs: 32-byte messages (offs == nullptr) or msgs[offs[i] .. offs[i+1]); status: items to skip (may be null)
+__global__ void __launch_bounds__(64) k_h2c_sswu_iso2(size_t B, const uint8_t* msgs, const uint64_t* offs,
+                                                      const int* status, Fd* hf, int* flag) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B) return;  // both lanes of an item leave together
+  Fd* o = hf + HCF * i + HCF_Q;
+  if (status && !status[i]) {
+    pp2_store(o, PP<Fp2>{fp2_zero(), fp2_zero(), fp2_zero()}, hi);
+    if (!hi) flag[i] = 0;
+    return;
+  }
+  Fp2 u[2];
+  if (offs)
+    hash_to_field_fp2(u, msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_FAV, 43);
+  else
+    hash_to_field_fp2(u, msgs + 32 * i, 32, DST_POP_FAV, 43);
+  Fp2 x, y;
+  map_to_curve_sswu_lane(x, y, hi ? u[1] : u[0]);
+  const PP<Fp2> mine = iso_proj_lane(x, y);
+  const PP<Fp2> other = pp2_swap(mine);
+  const uint32_t bad = fp2_is_zero(mine.z) ? 1u : 0u;  // an isogeny denominator vanished: k_h2c_fallback
+  const uint32_t any_bad = bad | cl_swap(bad);
+  const PP<Fp2> Q = pp2_add(pp2_sel(hi, other, mine), pp2_sel(hi, mine, other), hi);
+  pp2_store(o, Q, hi);
+  if (!hi) flag[i] = any_bad ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(64) k_g2x_pre2(size_t B, Fd* hf) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B) return;
+  Fd* r = hf + HCF * i;
+  const PP<Fp2> Q = pp2_load(r + HCF_Q);
+  const PP<Fp2> M = pp2_mul_xabs(Q, hi);
+  const PP<Fp2> pq = pp2_psi(Q);
+  const PP<Fp2> A = pp2_add(pq, pp2_neg(M), hi);                       // t1 + t2, t1 = -M
+  const PP<Fp2> t3 = pp2_psi2(pp2_dbl(Q, hi));                         // psi^2(2Q)
+  const PP<Fp2> C = pp2_add(pp2_add(t3, pp2_neg(pq), hi), pp2_add(M, pp2_neg(Q), hi), hi);
+  pp2_store(r + HCF_A, A, hi);
+  pp2_store(r + HCF_C, C, hi);
+}
+
+__global__ void __launch_bounds__(64) k_g2x_post2(size_t B, Fd* hf) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B) return;
+  Fd* r = hf + HCF * i;
+  const PP<Fp2> M = pp2_mul_xabs(pp2_load(r + HCF_A), hi);
+  const PP<Fp2> H = pp2_add(pp2_load(r + HCF_C), pp2_neg(M), hi);
+  pp2_store(r + HCF_A, H, hi);  // projective H over the dead A slots (k_h2c_affine reads them)
+}
+
+static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs,
+                                   const int* status, Fd* hf, G2A* H, int* flag) {
+  const dim3 g((unsigned)((2 * B + 63) / 64));
+  hipLaunchKernelGGL(k_h2c_sswu_iso2, g, dim3(64), 0, st, B, msgs, offs, status, hf, flag);
+  hipLaunchKernelGGL(k_g2x_pre2, g, dim3(64), 0, st, B, hf);
+  hipLaunchKernelGGL(k_g2x_post2, g, dim3(64), 0, st, B, hf);
+  hipLaunchKernelGGL(k_h2c_affine, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, status, hf, H);
+  return hipGetLastError();
+}
+// A/B knob: BLS_H2C_VM=1 runs SSWU + the wave-program phases (k_h2c_iso / _pre / _post)
+static bool h2c_use_vm() {
+  static const bool vm = getenv("BLS_H2C_VM") != nullptr;
+  return vm;
+}
+
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 static int env_int_or(const char* name, int dflt) {
   const char* v = getenv(name);
@@ -356,6 +496,7 @@ static hipError_t launch_h2c_phases(hipStream_t st, size_t B, const int* status,
 hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
                       int* flag) {
   if (!B) return hipSuccess;
+  if (!h2c_use_vm()) return launch_h2c_lane2(st, B, msgs32, nullptr, status, hf, H, flag);
   hipLaunchKernelGGL(k_h2c_sswu, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs32, status, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -370,6 +511,7 @@ hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int
 hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U, Fd* hf,
                            G2A* H, int* flag) {
   if (!B) return hipSuccess;
+  if (!h2c_use_vm()) return launch_h2c_lane2(st, B, msgs, offs, nullptr, hf, H, flag);
   hipLaunchKernelGGL(k_h2c_sswu_var, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, U);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

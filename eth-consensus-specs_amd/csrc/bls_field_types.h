@@ -26,6 +26,18 @@ struct alignas(16) Fp {
 struct alignas(16) Fd {
   uint32_t d[20];
 };
+// Lane-kernel form of an Fp value (bls_fq.h): 14 digits of radix 2^28,
+// Montgomery radix R' = 2^392, redundant (digits may exceed 2^28 and the value
+// p) -- additions and subtractions are digit-wise with no carry chain.
+struct Fq {
+  uint32_t d[14];
+};
+struct Fq2 {
+  Fq c0, c1;
+};
+struct Fq6 {
+  Fq2 c0, c1, c2;
+};
 struct Fp2 {
   Fp c0, c1;  // c0 + c1 * i,  i^2 = -1
 };

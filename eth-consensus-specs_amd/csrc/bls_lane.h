@@ -5,8 +5,8 @@
 //     exponents cost ~379 squarings + ~95 products with operands in VGPRs;
 //   - fp2_sqrt_lane: square root in Fp2 with two Fp exponentiations and no
 //     inversion or Jacobi symbol (see below);
-//   - map_to_curve_sswu_lane: RFC 9380 simplified SWU whose second square
-//     root needs only one exponentiation (its norm root is derived);
+//   - map_to_curve_sswu_lane: RFC 9380 simplified SWU with two exponentiations
+//     (x1's inversion is folded into the norm root's, see below);
 //   - g2_decompress_lane: ZCash signature decoding with fp2_sqrt_lane.
 // Results are identical to bls_h2c.h / bls_curve.h (the same canonical
 // points; tests/hostcheck compares both with the oracle).
@@ -95,27 +95,48 @@ BLS_HD int fp2_sgn0_lane(const Fp2& a_mont) {
   return (int)(a0.l[0] & 1u) | ((int)fp_is_zero(a0) & (int)(a1.l[0] & 1u));
 }
 
-// RFC 9380 simplified SWU on E2' -> affine (x, y).  If g(x1) is not a square,
-// g(x2) = Z^3 u^6 g(x1) and c = norm(g(x1))^((p+1)/4) satisfies
-// c^2 = -norm(g(x1)), so norm(g(x2)) has the root K c norm(u)^3 with
-// K = sqrt(-norm(Z)^3) (SSWU_K_NORM): one exponentiation saved.
+// RFC 9380 simplified SWU on E2' -> affine (x, y), with ONE exponentiation
+// before the final square root instead of an inversion plus an
+// exponentiation.  x1 = xn / xd (xn = -B/A (den + 1), xd = den), D = norm(xd),
+// g(x1) = gxn / xd^3 and norm(g(x1)) = Ag / D^3 with Ag = norm(gxn).  For
+// w = Ag D^5 and z = w^((p-3)/4) (p = 3 mod 4), z^2 = chi(w) / w, where
+// chi(w) = chi(norm(g(x1))) says whether g(x1) is a square in Fp2.  Hence
+//   1 / D = chi z^2 Ag D^4      (the inversion of x1)
+//   c = Ag D z,  c^2 = chi norm(g(x1))
+// -- c is a root of +-norm(g(x1)), which is all the two branches below need
+// (round 1 took c = norm(g(x1))^((p+1)/4), the same up to sign; the root's sign
+// does not matter to fp2_sqrt_from_norm_root, and y's sign is fixed by sgn0).
+// If g(x2) is used, g(x2) = Z^3 u^6 g(x1) and its norm root is K c norm(u)^3
+// with K = sqrt(-norm(Z)^3) (SSWU_K_NORM).  Ag = 0 (g(x1) = 0) keeps 1/D by a
+// Fermat inversion (unreachable for hash outputs in practice).
 BLS_HDNI void map_to_curve_sswu_lane(Fp2& x, Fp2& y, const Fp2& u) {
   const Fp2 u2 = fp2_sqr(u);
   const Fp2 zu2 = fp2_mul(SSWU_Z, u2);
   const Fp2 den = fp2_add(fp2_sqr(zu2), zu2);
-#ifndef BLS_SSWU_GCD
-  const Fp2 x1 = fp2_is_zero(den) ? SSWU_B_OVER_ZA : fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv_lane(den)));
-#else
-  const Fp2 x1 = fp2_is_zero(den) ? SSWU_B_OVER_ZA : fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), fp2_inv(den)));
-#endif
-  const Fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
-  const Fp nrm1 = fp_add(fp_sqr_i(gx1.c0), fp_sqr_i(gx1.c1));
-  const Fp c = fp_sqrt_cand(nrm1);
+  const bool exc = fp2_is_zero(den);
+  const Fp2 xn = exc ? SSWU_B_OVER_ZA : fp2_mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), den));
+  const Fp2 xd = exc ? fp2_one() : den;
+  const Fp2 xd2 = fp2_sqr(xd);
+  // gxn = xn^3 + A xn xd^2 + B xd^3
+  const Fp2 gxn = fp2_add(fp2_mul(fp2_add(fp2_sqr(xn), fp2_mul(SSWU_A, xd2)), xn), fp2_mul(SSWU_B, fp2_mul(xd2, xd)));
+  const Fp ag = fp_add(fp_sqr_i(gxn.c0), fp_sqr_i(gxn.c1));
+  const Fp d = fp_add(fp_sqr_i(xd.c0), fp_sqr_i(xd.c1));
+  const Fp d2 = fp_sqr_i(d), d4 = fp_sqr_i(d2);
+  const Fp w = fp_mul_i(ag, fp_mul_i(d4, d));
+  const Fp z = fp_pow_pm3_4(w);
+  const Fp z2 = fp_sqr_i(z);
+  const bool square = fp_is_zero(ag) || fp_is_one(fp_mul_i(z2, w));  // chi(w) = 1 (or g(x1) = 0: y = 0)
+  Fp dinv = fp_mul_i(fp_mul_i(z2, ag), d4);  // chi / D
+  if (!square) dinv = fp_neg(dinv);
+  if (fp_is_zero(ag)) dinv = fp_inv_fermat_w3(d);
+  const Fp2 xnc = fp2_mul(xn, fp2_conj(xd));
+  const Fp2 x1{fp_mul_i(xnc.c0, dinv), fp_mul_i(xnc.c1, dinv)};
+  const Fp c = fp_mul_i(fp_mul_i(ag, d), z);
   Fp2 gx;
   Fp n;
-  if (fp_eq(fp_sqr_i(c), nrm1)) {
+  if (square) {
     x = x1;
-    gx = gx1;
+    gx = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), SSWU_A), x1), SSWU_B);
     n = c;
   } else {
     x = fp2_mul(zu2, x1);

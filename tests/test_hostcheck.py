@@ -232,9 +232,8 @@ def test_lane_chain_math():
     for a in ns:
         ok, _ = H.call("hc_fp2_sqrt_lane", H.fp2_b(a), out=96, ret=True)
         assert ok == 0
-    # SSWU: both branches (g(x1) square or not) over random inputs
-    for _ in range(12):
-        u = rfp2()
+    # SSWU: both branches (g(x1) square or not) over random inputs, and u = 0 (x1's denominator vanishes)
+    for u in [rfp2() for _ in range(16)] + [(0, 0), (1, 0), (0, 1)]:
         out = H.call("hc_map_to_curve_lane", H.fp2_b(u), out=192)
         assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
     # decompression incl. both y signs
