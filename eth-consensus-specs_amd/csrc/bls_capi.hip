@@ -857,11 +857,11 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   // 5 (default): lines on stream2, f accumulated by k_miller_acc4<2> (four lanes per f, two pairs per f:
   // one squaring per step for both; measured 1.31M FAV/s against 1.29M for acc4 and 1.16M for acc2);
   // A/B knobs: BLS_ML_MODE=acc4 (four lanes, one pair per f), acc2 (k_miller_acc2, two lanes per pair),
-  // acc1 (k_miller_acc, one lane per pair), st1 (both on stream1), fused (k_miller_lane)
+  // acc1 (k_miller_acc, one lane per pair), st1 (both on stream1), fused (k_miller_lane), acc4g4 (four pairs per f)
   static const int ml_mode = [] {
     const char* m = getenv("BLS_ML_MODE");
     return !m ? 5 : !strcmp(m, "fused") ? 0 : !strcmp(m, "st1") ? 1 : !strcmp(m, "acc1") ? 2 : !strcmp(m, "acc2") ? 3
-                  : !strcmp(m, "acc4") ? 4 : 5;
+                  : !strcmp(m, "acc4") ? 4 : !strcmp(m, "acc4g4") ? 6 : 5;
   }();
   uint32_t* mlines = nullptr;
   if (ml_mode) SCR(S_MLINES, miller_lines_u32(B), mlines);
@@ -918,7 +918,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     if (ml_mode == 1) PROF(12, launch_miller_lines(st, H, B, mlines));
     size_t nf = B;  // Miller values to multiply
     if (ml_mode >= 4) {
-      const int G = ml_mode == 5 ? 2 : 1;
+      const int G = ml_mode == 6 ? 4 : ml_mode == 5 ? 2 : 1;
       PROF(5, launch_miller_acc4(st, rP, H, status, B, mlines, f, G));
       nf = (B + G - 1) / G;
     } else if (ml_mode == 3)

@@ -158,11 +158,76 @@ __global__ void __launch_bounds__(64) k_g2x_lane2(size_t B, Fd* hf, int src, int
   }
 }
 
+// k_sig_lane with the G2 chain on ONE lane per item in Jacobian coordinates
+// (bls_pp_lane.h j2_dbl / j2_add_aff: 16 FME per doubling and item against
+// 2 x 12 on a lane pair).  Sigma is attacker-chosen, so the incomplete
+// addition's exceptional cases are real inputs: an item that raises one reruns
+// the complete projective chain (pp_dbl / pp_add_aff), a data-dependent branch
+// that only such inputs take.  Blocks [0, nb) run r_i apk_i, [nb, 2 nb) [|x|] sigma_i.
+__global__ void __launch_bounds__(64) k_sig_lane1j(size_t B, const int* gstat, int* status, const int* dstat,
+                                                   const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
+  const unsigned nb = (unsigned)((B + 63) / 64);
+  const bool g2 = blockIdx.x >= nb;
+  const size_t i = (size_t)(g2 ? blockIdx.x - nb : blockIdx.x) * 64 + threadIdx.x;
+  if (i >= B) return;
+  const bool live = gstat[i] && dstat[i];
+  if (!g2) {
+    if (!live) return;
+    const G1P a = apk[i];
+    const PP<Fp> A{a.x, a.y, a.z};
+    const uint64_t r = rsc[i];
+    PP<Fp> R{fp_zero(), FP_ONE, fp_zero()};
+    if ((r >> 63) & 1ull) R = A;
+#pragma unroll 1
+    for (int b = 62; b >= 0; --b) {
+      R = pp_dbl(R);
+      if ((r >> b) & 1ull) R = pp_add(R, A);
+    }
+    rPj[i] = G1P{R.x, R.y, R.z};
+    return;
+  }
+  if (!live) {
+    status[i] = 0;
+    return;
+  }
+  const G2A s = sig[i];
+  bool exc = false;
+  G2J M{s.x, s.y, fp2_one()};
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    M = j2_dbl(M);
+    if ((X_ABS >> b) & 1ull) M = j2_add_aff(M, s.x, s.y, exc);
+  }
+  // sigma in G2  <=>  psi(sigma) == -M with M not the identity; psi(sigma) = (conj(x) cx, conj(y) cy) affine
+  const Fp2 px = f2mul(fp2_conj(s.x), PSI_CX), py = f2mul(fp2_conj(s.y), PSI_CY);
+  bool ok;
+  if (!exc) {
+    const Fp2 zz = f2sqr(M.z);
+    ok = fp2_is_zero(fp2_sub(f2mul(px, zz), M.x)) && fp2_is_zero(fp2_add(f2mul(py, f2mul(zz, M.z)), M.y)) &&
+         !fp2_is_zero(M.z);
+  } else {  // complete formulas (k_sig_lane)
+    PP<Fp2> P{s.x, s.y, fp2_one()};
+#pragma unroll 1
+    for (int b = 62; b >= 0; --b) {
+      P = pp_dbl(P);
+      if ((X_ABS >> b) & 1ull) P = pp_add_aff(P, s.x, s.y);
+    }
+    ok = fp2_is_zero(fp2_sub(f2mul(px, P.z), P.x)) && fp2_is_zero(fp2_add(f2mul(py, P.z), P.y)) &&
+         !fp2_is_zero(P.z);
+  }
+  status[i] = ok ? 1 : 0;
+}
+
 hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
                            const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   if (!B) return hipSuccess;
-  static const bool one_lane = getenv("BLS_SIG1") != nullptr;  // A/B knob: k_sig_lane (one lane per G2 chain)
-  if (one_lane)
+  // A/B knobs: BLS_SIG1 = k_sig_lane (one lane per G2 chain, complete formulas), BLS_SIG1J = k_sig_lane1j (one
+  // lane, Jacobian; 1.41-1.43M FAV/s against 1.43-1.50M for the lane pairs: its 512 registers still spill)
+  static const bool one_lane = getenv("BLS_SIG1") != nullptr, jac = getenv("BLS_SIG1J") != nullptr;
+  if (jac)
+    hipLaunchKernelGGL(k_sig_lane1j, dim3(2 * (unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat,
+                       apk, sig, rsc, rPj);
+  else if (one_lane)
     hipLaunchKernelGGL(k_sig_lane, dim3(2 * (unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat, apk,
                        sig, rsc, rPj);
   else

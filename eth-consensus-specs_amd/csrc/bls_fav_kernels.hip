@@ -443,12 +443,101 @@ __global__ void __launch_bounds__(64) k_g2x_post2(size_t B, Fd* hf) {
   pp2_store(r + HCF_A, H, hi);  // projective H over the dead A slots (k_h2c_affine reads them)
 }
 
+// The cofactor-clearing chains on ONE lane per item in Jacobian coordinates
+// (bls_pp_lane.h j2_*: 16 instead of 2 x 12 FME per doubling and item); the
+// pre/post steps stay complete projective (pp_add).  An exceptional case of
+// the incomplete chain additions raises flag[i], and k_h2c_fallback recomputes
+// the item with the reference-path formulas.  Items with status 0 are skipped.
+__device__ __forceinline__ PP<Fp2> pp_neg2(const PP<Fp2>& p) { return PP<Fp2>{p.x, fp2_neg(p.y), p.z}; }
+__device__ __forceinline__ PP<Fp2> pp_psi2x(const PP<Fp2>& p) {
+  return PP<Fp2>{f2mul(fp2_conj(p.x), PSI_CX), f2mul(fp2_conj(p.y), PSI_CY), fp2_conj(p.z)};
+}
+__device__ __forceinline__ void pp_store1(Fd* o, const PP<Fp2>& p) {
+  o[0] = fd_from_fp(p.x.c0);
+  o[1] = fd_from_fp(p.x.c1);
+  o[2] = fd_from_fp(p.y.c0);
+  o[3] = fd_from_fp(p.y.c1);
+  o[4] = fd_from_fp(p.z.c0);
+  o[5] = fd_from_fp(p.z.c1);
+}
+
+__global__ void __launch_bounds__(64) k_g2x_pre1(size_t B, const int* status, Fd* hf, int* flag) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || (status && !status[i])) return;
+  Fd* r = hf + HCF * i;
+  const PP<Fp2> Q = pp2_load(r + HCF_Q);
+  bool exc = false;
+  const PP<Fp2> M = j2_to_pp(j2_mul_xabs(j2_from_pp(Q), exc));
+  const PP<Fp2> pq = pp_psi2x(Q);
+  pp_store1(r + HCF_A, pp_add(pq, pp_neg2(M)));  // t1 + t2, t1 = -M
+  const PP<Fp2> mq = pp_add(M, pp_neg2(Q));
+  const PP<Fp2> t3{f2mul(Q.x, PSI2_CX), f2mul(Q.y, PSI2_CY), Q.z};  // psi^2(Q); psi^2(2Q) = 2 psi^2(Q)
+  pp_store1(r + HCF_C, pp_add(pp_add(pp_dbl(t3), pp_neg2(pq)), mq));
+  if (exc) flag[i] = 1;
+}
+
+__global__ void __launch_bounds__(64) k_g2x_post1(size_t B, const int* status, Fd* hf, int* flag) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || (status && !status[i])) return;
+  Fd* r = hf + HCF * i;
+  bool exc = false;
+  const PP<Fp2> M = j2_to_pp(j2_mul_xabs(j2_from_pp(pp2_load(r + HCF_A)), exc));
+  pp_store1(r + HCF_A, pp_add(pp2_load(r + HCF_C), pp_neg2(M)));  // projective H over the dead A slots
+  if (exc) flag[i] = 1;
+}
+
+// The same split into lean kernels: the one-lane Jacobian chain alone (its
+// register budget is the chain's), and the pre/post steps on lane pairs.
+__global__ void __launch_bounds__(64) k_g2x_j1(size_t B, const int* status, Fd* hf, int src, int dst, int* flag) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || (status && !status[i])) return;
+  Fd* r = hf + HCF * i;
+  bool exc = false;
+  pp_store1(r + dst, j2_to_pp(j2_mul_xabs(j2_from_pp(pp2_load(r + src)), exc)));
+  if (exc) flag[i] = 1;
+}
+__global__ void __launch_bounds__(64) k_h2c_pre_pair(size_t B, Fd* hf) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B) return;
+  Fd* r = hf + HCF * i;
+  const PP<Fp2> Q = pp2_load(r + HCF_Q), M = pp2_load(r + HCF_M);
+  const PP<Fp2> pq = pp2_psi(Q);
+  pp2_store(r + HCF_A, pp2_add(pq, pp2_neg(M), hi), hi);
+  const PP<Fp2> t3 = pp2_psi2(pp2_dbl(Q, hi));
+  pp2_store(r + HCF_C, pp2_add(pp2_add(t3, pp2_neg(pq), hi), pp2_add(M, pp2_neg(Q), hi), hi), hi);
+}
+__global__ void __launch_bounds__(64) k_h2c_post_pair(size_t B, Fd* hf) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B) return;
+  Fd* r = hf + HCF * i;
+  pp2_store(r + HCF_A, pp2_add(pp2_load(r + HCF_C), pp2_neg(pp2_load(r + HCF_M)), hi), hi);
+}
+
 static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs,
                                    const int* status, Fd* hf, G2A* H, int* flag) {
   const dim3 g((unsigned)((2 * B + 63) / 64));
   hipLaunchKernelGGL(k_h2c_sswu_iso2, g, dim3(64), 0, st, B, msgs, offs, status, hf, flag);
-  hipLaunchKernelGGL(k_g2x_pre2, g, dim3(64), 0, st, B, hf);
-  hipLaunchKernelGGL(k_g2x_post2, g, dim3(64), 0, st, B, hf);
+  // default: one-lane Jacobian chains fused with pre/post (k_g2x_pre1 / _post1).  A/B knobs (interleaved medians,
+  // profiles/r02o_h2c_chains_ab.txt): BLS_H2C_SPLIT = one-lane chains alone + lane-pair pre/post kernels (1.465M
+  // FAV/s against 1.482M), BLS_H2C_CHAIN2 = lane-pair complete-formula chains fused with pre/post (1.437M)
+  static const bool pair_chains = getenv("BLS_H2C_CHAIN2") != nullptr, split = getenv("BLS_H2C_SPLIT") != nullptr;
+  const dim3 g1((unsigned)((B + 63) / 64));
+  if (split) {
+    hipLaunchKernelGGL(k_g2x_j1, g1, dim3(64), 0, st, B, status, hf, HCF_Q, HCF_M, flag);
+    hipLaunchKernelGGL(k_h2c_pre_pair, g, dim3(64), 0, st, B, hf);
+    hipLaunchKernelGGL(k_g2x_j1, g1, dim3(64), 0, st, B, status, hf, HCF_A, HCF_M, flag);
+    hipLaunchKernelGGL(k_h2c_post_pair, g, dim3(64), 0, st, B, hf);
+  } else if (pair_chains) {
+    hipLaunchKernelGGL(k_g2x_pre2, g, dim3(64), 0, st, B, hf);
+    hipLaunchKernelGGL(k_g2x_post2, g, dim3(64), 0, st, B, hf);
+  } else {
+    hipLaunchKernelGGL(k_g2x_pre1, g1, dim3(64), 0, st, B, status, hf, flag);
+    hipLaunchKernelGGL(k_g2x_post1, g1, dim3(64), 0, st, B, status, hf, flag);
+  }
   hipLaunchKernelGGL(k_h2c_affine, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, status, hf, H);
   return hipGetLastError();
 }

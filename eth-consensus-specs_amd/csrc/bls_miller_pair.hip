@@ -374,7 +374,9 @@ hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const 
   if (!n) return hipSuccess;
   const size_t ngrp = (n + G - 1) / G;
   const dim3 grid((unsigned)((4 * ngrp + 63) / 64));
-  if (G == 2)
+  if (G == 4)
+    hipLaunchKernelGGL(k_miller_acc4<4>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
+  else if (G == 2)
     hipLaunchKernelGGL(k_miller_acc4<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
   else
     hipLaunchKernelGGL(k_miller_acc4<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);

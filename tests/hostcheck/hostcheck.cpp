@@ -6,6 +6,7 @@
 #include "bls_ops.h"
 #include "bls_lane.h"
 #include "bls_tower_inline.h"
+#include "bls_pp_lane.h"
 #include <string.h>
 using namespace bls;
 
@@ -108,3 +109,26 @@ extern "C" int hc_g2_decompress_lane(const uint8_t* b, uint8_t* o) {
   return st;
 }
 extern "C" void hc_fp_pow_w3(const uint8_t* a, const uint32_t* e, int nbits, uint8_t* o) { out_fp(o, fp_pow_w3(in_fp(a), e, nbits)); }
+
+// Jacobian [|x|] chain of the hash_to_G2 lane kernels (bls_pp_lane.h j2_*), from and back to homogeneous
+// projective: q affine (x0||x1||y0||y1, 192 bytes) -> affine [|x|] q; returns the exception flag
+extern "C" int hc_j2_mul_xabs(const uint8_t* q, uint8_t* o) {
+  const PP<Fp2> Q{in_fp2(q), in_fp2(q + 96), fp2_one()};
+  bool exc = false;
+  const PP<Fp2> M = j2_to_pp(j2_mul_xabs(j2_from_pp(Q), exc));
+  const Fp2 zi = fp2_inv(M.z);
+  out_fp2(o, fp2_mul(M.x, zi));
+  out_fp2(o + 96, fp2_mul(M.y, zi));
+  return exc ? 1 : 0;
+}
+// madd chain step: affine p + affine q through j2_add_aff (p as Jacobian with Z = 1)
+extern "C" int hc_j2_add_aff(const uint8_t* p, const uint8_t* q, uint8_t* o) {
+  const G2J P{in_fp2(p), in_fp2(p + 96), fp2_one()};
+  bool exc = false;
+  const G2J R = j2_add_aff(j2_dbl(P), in_fp2(q), in_fp2(q + 96), exc);  // 2p + q
+  const PP<Fp2> S = j2_to_pp(R);
+  const Fp2 zi = fp2_inv(S.z);
+  out_fp2(o, fp2_mul(S.x, zi));
+  out_fp2(o + 96, fp2_mul(S.y, zi));
+  return exc ? 1 : 0;
+}

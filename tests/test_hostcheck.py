@@ -242,3 +242,21 @@ def test_lane_chain_math():
         for pt in (q, O.g2_neg(q)):
             st, out = H.call("hc_g2_decompress_lane", O.g2_compress(pt), out=192, ret=True)
             assert st == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == pt
+
+
+def test_jacobian_lane_chains():
+    """j2_* (bls_pp_lane.h): [|x|] Q through the Jacobian chain of the hash_to_G2 lane kernels, and the
+    affine-input addition, against the oracle; the identity input raises the exception flag."""
+    for k in (1, 7, 0x5EED):
+        q = O.g2_mul(O.G2_GEN, k)
+        exc, out = H.call("hc_j2_mul_xabs", H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192, ret=True)
+        assert exc == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.g2_mul(q, O.X_ABS)
+        p = O.g2_mul(O.G2_GEN, k + 3)
+        exc, out = H.call("hc_j2_add_aff", H.fp2_b(p[0]) + H.fp2_b(p[1]), H.fp2_b(q[0]) + H.fp2_b(q[1]),
+                          out=192, ret=True)
+        assert exc == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.g2_add(O.g2_mul(p, 2), q)
+    # 2p + q with q = -2p: h = 0, flagged
+    p = O.g2_mul(O.G2_GEN, 5)
+    q = O.g2_neg(O.g2_mul(p, 2))
+    exc, _ = H.call("hc_j2_add_aff", H.fp2_b(p[0]) + H.fp2_b(p[1]), H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192, ret=True)
+    assert exc == 1

@@ -1,14 +1,28 @@
 #!/bin/bash
-# A/B of env knobs: each argument is a space-separated "VAR=VALUE ..." set (or "base"), one 40-step bench each.
-# Usage (via gpurun): bash tools/knob_ab.sh TAG "base" "BLS_XC_G=1" "BLS_XC_G=1 BLS_FAV_JOBS_INIT=6" ...
+# A/B of env knobs: each argument is a space-separated "VAR=VALUE ..." set (or "base").  The sets run
+# interleaved REPS times (default 3), STEPS timed passes each (default 60); the median per set is printed.
+# Usage (via gpurun): REPS=3 bash tools/knob_ab.sh TAG "base" "BLS_XC_G=1" ...
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
+REPS=${REPS:-3}; STEPS=${STEPS:-60}
+for r in $(seq 1 $REPS); do
+  i=0
+  for kv in "$@"; do
+    i=$((i+1))
+    envs=""; [ "$kv" != base ] && envs="$kv"
+    env $envs timeout -k 10 150 python3 bench.py --steps $STEPS --warmup 3 --no-cpu --no-percall --no-e2e --roofline-passes 2 \
+      > $OUT/k${i}_r$r.json 2> $OUT/k${i}_r$r.err || { echo "[$kv] FAILED rc=$?"; tail -3 $OUT/k${i}_r$r.err | cut -c1-300; exit 1; }
+    python3 -c "import json; d=json.load(open('$OUT/k${i}_r$r.json')); print('[$kv] r$r', d['value'])"
+  done
+done
 i=0
 for kv in "$@"; do
   i=$((i+1))
-  envs=""; [ "$kv" != base ] && envs="$kv"
-  env $envs timeout -k 10 150 python3 bench.py --steps 40 --warmup 3 --no-cpu --no-percall --no-e2e \
-    > $OUT/k$i.json 2> $OUT/k$i.err || { echo "[$kv] FAILED rc=$?"; tail -3 $OUT/k$i.err | cut -c1-300; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/k$i.json')); k=d['kernels_avg_ms']; print('[$kv]', d['value'], 'miller', k['miller'], 'hash', k['fav_hash'], 'frac', d['roofline']['frac'])"
+  python3 - "$OUT" "$i" "$kv" <<'PY'
+import glob, json, statistics, sys
+out, i, kv = sys.argv[1:]
+v = sorted(json.load(open(f))["value"] for f in glob.glob(f"{out}/k{i}_r*.json"))
+print(f"[{kv}] median {statistics.median(v):.0f}  all {[round(x) for x in v]}")
+PY
 done
