@@ -12,7 +12,10 @@
 // runs on its own high-priority stream beside the Miller loops of the
 // (r_i apk_i, H_i) pairs.
 #include "bls_kernels.h"
+#include "bls_pp_lane.h"
 #include "bls_vm.h"
+
+#include <stdlib.h>
 
 namespace bls {
 
@@ -141,6 +144,61 @@ __global__ void __launch_bounds__(64) k_msm_tree(const Fd* in, int nout, int k, 
   }
 }
 
+// ----------------------------------------------------------- lane form --
+// The bucket sums and both reduction trees on lane pairs (bls_pp_lane.h pp2_*)
+// instead of wave programs: a bucket is ~40 sequential mixed additions, a tree
+// node one addition (after k doublings), so a 64-lane workgroup spent most of
+// its time staging slots and on per-level barriers for 4 items.  Same points
+// in the same projective form (complete formulas), same Fd staging.
+namespace {
+__device__ __forceinline__ PP<Fp2> msm_load(const Fd* in) {
+  return PP<Fp2>{Fp2{fp_from_fd(in[0]), fp_from_fd(in[1])}, Fp2{fp_from_fd(in[2]), fp_from_fd(in[3])},
+                 Fp2{fp_from_fd(in[4]), fp_from_fd(in[5])}};
+}
+__device__ __forceinline__ void msm_store(Fd* o, const PP<Fp2>& p, bool hi) {
+  if (!hi) {
+    o[0] = fd_from_fp(p.x.c0);
+    o[1] = fd_from_fp(p.x.c1);
+    o[2] = fd_from_fp(p.y.c0);
+  } else {
+    o[3] = fd_from_fp(p.y.c1);
+    o[4] = fd_from_fp(p.z.c0);
+    o[5] = fd_from_fp(p.z.c1);
+  }
+}
+}  // namespace
+
+// bucket b = (lane pair index): bsum[b] = sum of its points (identity (0 : 1 : 0) if empty)
+__global__ void __launch_bounds__(64) k_msm_bucket2(const uint32_t* off, const uint32_t* lst, const G2A* sig,
+                                                    Fd* bsum) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  const int b = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (b >= MSM_NB) return;
+  PP<Fp2> R{fp2_zero(), fp2_one(), fp2_zero()};
+  const uint32_t lo = off[b], hi_end = off[b + 1];
+  // both lanes of a pair run the same trip count (the pair's bucket)
+#pragma unroll 1
+  for (uint32_t k = lo; k < hi_end; ++k) {
+    const G2A& q = sig[lst[k]];
+    R = pp2_add_aff(R, q.x, q.y, hi);
+  }
+  msm_store(bsum + (size_t)b * 6, R, hi);
+}
+
+// out[j] = in[2j] + [2^k] in[2j+1] (k = 0: plain sum), one lane pair per output
+__global__ void __launch_bounds__(64) k_msm_tree2(const Fd* in, int nout, int k, Fd* out) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  const int j = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (j >= nout) return;
+  const PP<Fp2> A = msm_load(in + (size_t)(2 * j) * 6);
+  PP<Fp2> Bp = msm_load(in + (size_t)(2 * j + 1) * 6);
+#pragma unroll 1
+  for (int s = 0; s < k; ++s) Bp = pp2_dbl(Bp, hi);
+  msm_store(out + (size_t)j * 6, pp2_add(A, Bp, hi), hi);
+}
+
 // projective S -> affine (identity if Z = 0)
 __global__ void __launch_bounds__(64) k_msm_affine(const Fd* pt, G2A* out) {
   __shared__ Fd s[WP_NCONST + WL_MA_STRIDE];
@@ -191,7 +249,12 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
     hipLaunchKernelGGL(k_msm_scatter, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cur, lst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_msm_bucket<MSM_G>, dim3(MSM_NB / MSM_G), dim3(64), 0, st, off, lst, sig, bsum);
+  // A/B knob: BLS_MSM_VM=1 runs the bucket sums and trees as wave programs (k_msm_bucket<4>, k_msm_tree<4>)
+  static const bool vm = getenv("BLS_MSM_VM") != nullptr;
+  if (vm)
+    hipLaunchKernelGGL(k_msm_bucket<MSM_G>, dim3(MSM_NB / MSM_G), dim3(64), 0, st, off, lst, sig, bsum);
+  else
+    hipLaunchKernelGGL(k_msm_bucket2, dim3(2 * MSM_NB / 64), dim3(64), 0, st, off, lst, sig, bsum);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_gather_bits, dim3(64 * 128 * 6 / 256), dim3(256), 0, st, bsum, ping);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -199,7 +262,10 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   Fd* a = ping;
   Fd* b = pong;
   for (int n = 64 * 64; n >= 64; n >>= 1) {
-    hipLaunchKernelGGL(k_msm_tree<4>, dim3((n + 3) / 4), dim3(64), 0, st, a, n, 0, b);
+    if (vm)
+      hipLaunchKernelGGL(k_msm_tree<4>, dim3((n + 3) / 4), dim3(64), 0, st, a, n, 0, b);
+    else
+      hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, 0, b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     Fd* t = a;
     a = b;
@@ -208,7 +274,10 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   // weighted tree: sum_b 2^b U_b, 64 -> 1
   int k = 1;
   for (int n = 32; n >= 1; n >>= 1, k <<= 1) {
-    hipLaunchKernelGGL(k_msm_tree<4>, dim3((n + 3) / 4), dim3(64), 0, st, a, n, k, b);
+    if (vm)
+      hipLaunchKernelGGL(k_msm_tree<4>, dim3((n + 3) / 4), dim3(64), 0, st, a, n, k, b);
+    else
+      hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, k, b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     Fd* t = a;
     a = b;
