@@ -26,9 +26,9 @@ struct alignas(16) Fp {
 struct alignas(16) Fd {
   uint32_t d[20];
 };
-// Lane-kernel form of an Fp value (bls_fq.h): 14 digits of radix 2^28,
-// Montgomery radix R' = 2^392, redundant (digits may exceed 2^28 and the value
-// p) -- additions and subtractions are digit-wise with no carry chain.
+// Lane-kernel form of an Fp value (bls_fq.h): 14 digits of radix 2^29, the
+// same Montgomery radix R = 2^406, redundant (digits may exceed 2^29 and the
+// value p) -- additions and subtractions are digit-wise with no carry chain.
 struct Fq {
   uint32_t d[14];
 };

@@ -5,6 +5,7 @@
 #include <cstdlib>
 
 #include "bls_kernels.h"
+#include "bls_fq_g1.h"
 
 namespace bls {
 
@@ -302,6 +303,63 @@ __global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const ui
   }
 }
 
+// The same gather in the redundant digit form: bls_fq_g1.h (g1q_add_aff, g1q_add).
+template <int L>
+__global__ void __launch_bounds__(64) k_fav_gather_q(const uint32_t* idx, const uint64_t* offs, size_t B,
+                                                     const RegKey* reg, uint32_t reg_n, G1P* apk, int* status) {
+  constexpr int IPW = 64 / L;
+  __shared__ G1Q sh[64];
+  __shared__ int bad[IPW];
+  const int sub = (int)threadIdx.x / L, ln = (int)threadIdx.x % L;
+  const size_t b = (size_t)blockIdx.x * IPW + sub;
+  if ((int)threadIdx.x < IPW) bad[threadIdx.x] = 0;
+  __syncthreads();
+  G1Q acc{fq_zero(), fq_unpack(FP_ONE), fq_zero()};  // identity (0 : 1 : 0)
+  int mybad = 0;
+  uint64_t lo = 0, hi = 0;
+  if (b < B) {
+    lo = offs[b];
+    hi = offs[b + 1];
+    for (uint64_t j = lo + ln; j < hi; j += L) {
+      const uint32_t k = idx[j];
+      if (k >= reg_n) {
+        mybad = 1;
+        continue;
+      }
+      const uint4* r = reinterpret_cast<const uint4*>(reg + k);
+      Fp x, y;
+      uint4* xv = reinterpret_cast<uint4*>(x.l);
+      uint4* yv = reinterpret_cast<uint4*>(y.l);
+      xv[0] = r[0];
+      xv[1] = r[1];
+      xv[2] = r[2];
+      yv[0] = r[3];
+      yv[1] = r[4];
+      yv[2] = r[5];
+      if (!(x.l[11] & REG_VALID)) {
+        mybad = 1;
+      } else {
+        x.l[11] &= ~REG_VALID;
+        acc = g1q_add_aff(acc, fq_unpack(x), fq_unpack(y));
+      }
+    }
+  }
+  if (mybad) atomicOr(&bad[sub], 1);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+#pragma unroll 1
+  for (int s = L / 2; s > 0; s >>= 1) {
+    if (ln < s) sh[threadIdx.x] = g1q_add(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (ln == 0 && b < B) {  // canonical projective aggregate key; the identity is invalid (KeyValidate of the sum)
+    const G1Q& a = sh[threadIdx.x];
+    const G1P o{fq_pack(a.x), fq_pack(a.y), fq_pack(a.z)};
+    apk[b] = o;
+    status[b] = (hi > lo && !bad[sub] && !fp_is_zero(o.z)) ? 1 : 0;
+  }
+}
+
 // Registry entries from decoded keys (bls_registry_load / _append): the
 // KeyValidate verdict goes into x's spare top bit; valid[i] = 1/0 for the host.
 __global__ void __launch_bounds__(256) k_reg_pack(const G1A* a, const int* ok, size_t n, RegKey* reg, uint8_t* valid) {
@@ -566,7 +624,13 @@ hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t
   // committees are not huge (the per-lane chains stay short), else 64
   static const int forced = getenv("BLS_GATHER_L") ? atoi(getenv("BLS_GATHER_L")) : 0;
   int L = forced ? forced : (B >= 8192 ? 16 : 64);
-  if (L == 16)
+  // A/B knob: BLS_GATHER_PACKED=1 runs the packed-Fp gather (k_fav_gather)
+  static const bool packed = getenv("BLS_GATHER_PACKED") != nullptr;
+  if (!packed && L == 16)
+    LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
+  else if (!packed && L == 64)
+    LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
+  else if (L == 16)
     LAUNCH(k_fav_gather<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else if (L == 8)
     LAUNCH(k_fav_gather<8>, (unsigned)((B + 7) / 8), 64, st, idx, offs, B, reg, reg_n, apk, status);

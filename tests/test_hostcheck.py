@@ -260,3 +260,44 @@ def test_jacobian_lane_chains():
     q = O.g2_neg(O.g2_mul(p, 2))
     exc, _ = H.call("hc_j2_add_aff", H.fp2_b(p[0]) + H.fp2_b(p[1]), H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192, ret=True)
     assert exc == 1
+
+
+def test_fq_gather_formulas():
+    """Registry-gather additions in the redundant digit form (bls_fq_g1.h) with bls_fq.h's 128-bit column and
+    subtraction-precondition checks compiled in: sums of random keys (both accumulators, the tree addition, the
+    identity start) against the oracle, including a zero-sum (P + (-P)) and repeated keys."""
+    import ctypes
+    H.lib().hc_fq_gather.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
+    pts = [O.g1_mul(O.G1_GEN, rng.randrange(1, O.R)) for _ in range(40)]
+    cases = [(pts[:33], 20), (pts[:2], 1), (pts[:1], 0), (pts[:5], 5), ([pts[3], pts[3], pts[3]], 1),
+             ([pts[7], O.g1_neg(pts[7])], 1), ([pts[7], pts[8], O.g1_neg(pts[7])], 2)]
+    for pl, split in cases:
+        raw = b"".join(H.fp_b(p[0]) + H.fp_b(p[1]) for p in pl)
+        out = H.call("hc_fq_gather", raw, len(pl), split, out=96)
+        want = None
+        for p in pl:
+            want = p if want is None else O.g1_add(want, p)
+        if want is None:
+            assert out == bytes(96)
+        else:
+            assert (H.b_fp(out[:48]), H.b_fp(out[48:])) == (want[0], want[1])
+
+
+def test_fq_mul_worst_digits():
+    """The digit-form product on operands at the digit bounds the formulas rely on (2^30 on both sides, and
+    3 * 2^29 against 2^29 + 2^4), with the value kept below p R: result congruent to x y / 2^406, below 2p."""
+    import ctypes
+    f = H.lib().hc_fq_mul_digits
+    A = ctypes.c_uint32 * 14
+    R = 2 ** 406
+    for dx, dy in ((2 ** 30 - 2, 2 ** 30 + 32), (3 * 2 ** 29, 2 ** 29 + 16), (2 ** 29 - 1, 2 ** 29 - 1)):
+        for top in (0, 40, 200):
+            x = [dx] * 13 + [top]
+            y = [dy] * 13 + [top]
+            r = A()
+            f(A(*x), A(*y), r)
+            xv = sum(d << (29 * i) for i, d in enumerate(x))
+            yv = sum(d << (29 * i) for i, d in enumerate(y))
+            rv = sum(d << (29 * i) for i, d in enumerate(r))
+            assert rv % O.P == xv * yv * pow(R, -1, O.P) % O.P
+            assert rv < 2 * O.P and all(d < 2 ** 29 for d in list(r)[:13])
