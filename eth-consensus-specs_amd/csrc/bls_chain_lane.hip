@@ -9,6 +9,7 @@
 //                r_i apk_i (G1, 64-bit RLC scalar), one scalar bit per step
 //   k_g2x_lane   M = [|x|] B on the hash_to_G2 staging slots (cofactor clearing)
 #include "bls_kernels.h"
+#include "bls_fq_g1.h"
 #include "bls_pp_lane.h"
 #include "bls_vm.h"
 
@@ -92,20 +93,20 @@ __global__ void __launch_bounds__(64) k_g2x_lane(size_t B, Fd* hf, int src, int 
 __global__ void __launch_bounds__(64) k_sig_lane2(size_t B, const int* gstat, int* status, const int* dstat,
                                                   const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   const unsigned nb1 = (unsigned)((B + 63) / 64);
-  if (blockIdx.x < nb1) {
+  if (blockIdx.x < nb1) {  // r_i apk_i in the redundant digit form (bls_fq_g1.h), canonical output
     const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= B || !(gstat[i] && dstat[i])) return;
     const G1P a = apk[i];
-    const PP<Fp> A{a.x, a.y, a.z};
+    const G1Q A{fq_unpack(a.x), fq_unpack(a.y), fq_unpack(a.z)};
     const uint64_t r = rsc[i];
-    PP<Fp> R{fp_zero(), FP_ONE, fp_zero()};
+    G1Q R{fq_zero(), fq_unpack(FP_ONE), fq_zero()};
     if ((r >> 63) & 1ull) R = A;
 #pragma unroll 1
     for (int b = 62; b >= 0; --b) {
-      R = pp_dbl(R);
-      if ((r >> b) & 1ull) R = pp_add(R, A);
+      R = g1q_dbl(R);
+      if ((r >> b) & 1ull) R = g1q_add(R, A);
     }
-    rPj[i] = G1P{R.x, R.y, R.z};
+    rPj[i] = G1P{fq_pack(R.x), fq_pack(R.y), fq_pack(R.z)};
     return;
   }
   const size_t t = (size_t)(blockIdx.x - nb1) * 64 + threadIdx.x;

@@ -52,4 +52,20 @@ BLS_HD G1Q g1q_add(const G1Q& p, const G1Q& q) {
   return r;
 }
 
+// complete doubling (RCB alg. 9) of an L-form point; outputs X, Y < 4p, Z < 2p in L form
+BLS_HD G1Q g1q_dbl(const G1Q& p) {
+  const Fq t0 = fq_mul(p.y, p.y);
+  const Fq t1 = fq_mul(p.y, p.z);
+  const Fq t2 = fq_mul_small(fq_mul(p.z, p.z), 12);                 // 3b Z^2, < 24p
+  const Fq u = fq_mul(p.x, p.y);
+  const Fq z8 = fq_mul_small(t0, 8);
+  const Fq x3a = fq_mul(t2, z8);
+  G1Q r;
+  r.z = fq_mul(t1, z8);
+  const Fq w = fq_norm(fq_sub2(t0, fq_mul_small(t2, 3)));           // t0 - 3 t2 + 128p
+  r.y = fq_norm(fq_add(fq_mul(w, fq_add(t0, t2)), x3a));
+  r.x = fq_mul_small(fq_mul(w, u), 2);
+  return r;
+}
+
 }  // namespace bls

@@ -166,3 +166,22 @@ extern "C" void hc_fq_mul_digits(const uint32_t* x, const uint32_t* y, uint32_t*
   const Fq c = fq_mul(a, b);
   memcpy(r, c.d, 56);
 }
+
+// r * P by the digit-form double-and-add of k_sig_lane2 (bls_fq_g1.h g1q_dbl / g1q_add), 64-bit r; out affine
+extern "C" void hc_fq_g1_mul64(const uint8_t* p, uint64_t r, uint8_t* o) {
+  const G1Q A{fq_unpack(in_fp(p)), fq_unpack(in_fp(p + 48)), fq_unpack(FP_ONE)};
+  G1Q R{fq_zero(), fq_unpack(FP_ONE), fq_zero()};
+  if ((r >> 63) & 1ull) R = A;
+  for (int b = 62; b >= 0; --b) {
+    R = g1q_dbl(R);
+    if ((r >> b) & 1ull) R = g1q_add(R, A);
+  }
+  const Fp X = fq_pack(R.x), Y = fq_pack(R.y), Z = fq_pack(R.z);
+  if (fp_is_zero(Z)) {
+    memset(o, 0, 96);
+    return;
+  }
+  const Fp zi = fp_inv(Z);
+  out_fp(o, fp_mul(X, zi));
+  out_fp(o + 48, fp_mul(Y, zi));
+}

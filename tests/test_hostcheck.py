@@ -301,3 +301,15 @@ def test_fq_mul_worst_digits():
             rv = sum(d << (29 * i) for i, d in enumerate(r))
             assert rv % O.P == xv * yv * pow(R, -1, O.P) % O.P
             assert rv < 2 * O.P and all(d < 2 ** 29 for d in list(r)[:13])
+
+
+def test_fq_g1_scalar_chain():
+    """The r_i apk_i chain of k_sig_lane2 in the digit form (g1q_dbl / g1q_add, checked columns) against the
+    oracle for random 64-bit scalars, r = 1 and r = 2^63."""
+    import ctypes
+    H.lib().hc_fq_g1_mul64.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+    for r in [rng.getrandbits(64) | 1 for _ in range(6)] + [1, 1 << 63, (1 << 64) - 1]:
+        p = O.g1_mul(O.G1_GEN, rng.randrange(1, O.R))
+        out = H.call("hc_fq_g1_mul64", H.fp_b(p[0]) + H.fp_b(p[1]), r, out=96)
+        want = O.g1_mul(p, r)
+        assert (H.b_fp(out[:48]), H.b_fp(out[48:])) == (want[0], want[1])
