@@ -56,7 +56,7 @@ SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
 LANE_KERNELS = {"miller": 2, "miller_lines": 2, "sig_vm": 3}
 GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
 # profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
-KERNEL_SYMBOL = {"miller": "k_miller_acc4<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather<16>"}
+KERNEL_SYMBOL = {"miller": "k_miller_acc4<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 
 
