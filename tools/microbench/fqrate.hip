@@ -1,7 +1,8 @@
 // Microbenchmark: packed Fp (bls_fp.h, radix-2^29 products on 12-limb
-// operands) against the radix-2^28 digit form Fq (bls_fq.h), one dependent
+// operands) against the redundant digit form Fq (bls_fq.h), one dependent
 // chain per lane, for a lone product and for the Karatsuba Fp2 product with
-// its subtractions.  Run on the GPU box:
+// its subtractions.  (profiles/r02l_fqrate_microbench.txt was measured with
+// the first, radix-2^28 version of Fq; the product has the same shape.)  Run on the GPU box:
 //   hipcc --offload-arch=gfx950 -O3 -I eth-consensus-specs_amd/csrc tools/microbench/fqrate.hip -o /tmp/fqrate
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -44,7 +45,11 @@ __global__ void __launch_bounds__(64) k_fp2(uint32_t* out, int iters) {
 __global__ void __launch_bounds__(64) k_fq2(uint32_t* out, int iters) {
   Fq2 x{fq_unpack(seed_fp(blockIdx.x * 64 + threadIdx.x)), fq_unpack(seed_fp(3))};
   const Fq2 y{fq_unpack(seed_fp(7)), fq_unpack(seed_fp(9))};
-  for (int it = 0; it < iters; it++) x = fq2_norm(fq2_mul(x, y));
+  for (int it = 0; it < iters; it++) {
+    const Fq t0 = fq_mul(x.c0, y.c0), t1 = fq_mul(x.c1, y.c1);
+    const Fq t2 = fq_mul(fq_add(x.c0, x.c1), fq_add(y.c0, y.c1));
+    x = Fq2{fq_norm(fq_sub(t0, t1)), fq_norm(fq_sub2(t2, fq_add(t0, t1)))};
+  }
   out[(size_t)blockIdx.x * 64 + threadIdx.x] = x.c0.d[0] ^ x.c1.d[13];
 }
 
@@ -58,7 +63,7 @@ int main() {
     const char* name;
     void (*k)(uint32_t*, int);
     int fme;
-  } ks[] = {{"Fp  product (packed)", k_fp, 1}, {"Fq  product (radix 2^28)", k_fq, 1},
+  } ks[] = {{"Fp  product (packed)", k_fp, 1}, {"Fq  product (digit form)", k_fq, 1},
             {"Fp2 Karatsuba (packed)", k_fp2, 3}, {"Fq2 Karatsuba + norm", k_fq2, 3}};
   int grids[] = {1024, 2048, 4096};
   for (auto& k : ks) {
