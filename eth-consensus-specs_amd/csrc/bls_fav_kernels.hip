@@ -319,6 +319,92 @@ __global__ void __launch_bounds__(64) k_g1_affine(size_t B, const int* status, c
   rP[i] = o;
 }
 
+// ------------------------------------------------ batched affine conversion --
+// k_g1_affine / k_h2c_affine spend one inversion per item, and a 64-lane wave
+// pays a whole inversion's time whether one lane or all need it.  Here each
+// lane converts AFF_K items (item w * 64 AFF_K + lane + 64 k, so every load is
+// coalesced) with Montgomery's trick: prefix products of the K denominators,
+// ONE inversion, then two products per item walking back -- ~1/K of the
+// inversions' SIMD time.  A zero denominator (identity, or a skipped item)
+// enters the products as 1 and gets the same output as the one-item kernels.
+constexpr int AFF_K = 8;
+
+__global__ void __launch_bounds__(64) k_g1_affine_b(size_t B, const int* status, const G1P* rPj, G1A* rP) {
+  const size_t base = (size_t)blockIdx.x * 64 * AFF_K + threadIdx.x;
+  Fp pre[AFF_K];
+  bool zero[AFF_K];
+  Fp acc = FP_ONE;
+#pragma unroll
+  for (int k = 0; k < AFF_K; ++k) {
+    const size_t i = base + 64 * k;
+    const bool live = i < B && status[i];
+    const Fp z = live ? rPj[i].z : FP_ONE;
+    zero[k] = fp_is_zero(z);
+    acc = fp_mul_i(acc, zero[k] ? FP_ONE : z);
+    pre[k] = acc;
+  }
+  Fp inv = fp_inv(acc);  // 1 / (z_0 ... z_{K-1})
+#pragma unroll
+  for (int k = AFF_K - 1; k >= 0; --k) {
+    const size_t i = base + 64 * k;
+    if (i >= B) continue;
+    const bool live = status[i] != 0;
+    const Fp zk = live ? rPj[i].z : FP_ONE;
+    const Fp zi = k ? fp_mul_i(inv, pre[k - 1]) : inv;
+    if (k && !zero[k]) inv = fp_mul_i(inv, zk);
+    G1A o{fp_zero(), fp_zero(), true};
+    if (live) {
+      const G1P q = rPj[i];
+      const Fp zz = zero[k] ? fp_zero() : zi;  // fp_inv(0) = 0, as k_g1_affine
+      o = G1A{fp_mul_i(q.x, zz), fp_mul_i(q.y, zz), false};
+    }
+    rP[i] = o;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_h2c_affine_b(size_t B, const int* status, const Fd* hf, G2A* H) {
+  const size_t base = (size_t)blockIdx.x * 64 * AFF_K + threadIdx.x;
+  Fp pre[AFF_K];
+  bool zero[AFF_K];
+  Fp acc = FP_ONE;
+#pragma unroll
+  for (int k = 0; k < AFF_K; ++k) {
+    const size_t i = base + 64 * k;
+    Fp n = FP_ONE;
+    if (i < B && (!status || status[i])) {
+      const Fd* r = hf + HCF * i + HCF_A;
+      n = fp2_norm(Fp2{fp_from_fd(r[4]), fp_from_fd(r[5])});
+    } else if (i < B) {
+      n = fp_zero();  // skipped item: identity output
+    }
+    zero[k] = fp_is_zero(n);
+    acc = fp_mul_i(acc, zero[k] ? FP_ONE : n);
+    pre[k] = acc;
+  }
+  Fp inv = fp_inv(acc);
+#pragma unroll
+  for (int k = AFF_K - 1; k >= 0; --k) {
+    const size_t i = base + 64 * k;
+    if (i >= B) continue;
+    const Fd* r = hf + HCF * i + HCF_A;
+    const Fp2 Z{fp_from_fd(r[4]), fp_from_fd(r[5])};
+    const Fp ni = k ? fp_mul_i(inv, pre[k - 1]) : inv;  // 1 / norm(Z)
+    G2A h{fp2_zero(), fp2_zero(), true};
+    if (!zero[k]) {
+      inv = k ? fp_mul_i(inv, fp2_norm(Z)) : inv;
+      const Fp2 X{fp_from_fd(r[0]), fp_from_fd(r[1])}, Y{fp_from_fd(r[2]), fp_from_fd(r[3])};
+      const Fp2 zi{fp_mul_i(Z.c0, ni), fp_neg(fp_mul_i(Z.c1, ni))};
+      h = G2A{f2mul(X, zi), f2mul(Y, zi), false};
+    }
+    H[i] = h;
+  }
+}
+
+static bool affine_single() {  // A/B knob: BLS_AFF1=1 runs the one-item-per-lane affine kernels
+  static const bool one = getenv("BLS_AFF1") != nullptr;
+  return one;
+}
+
 // ---------------------------------------------- hash_to_G2 on lane pairs --
 // The phases after SSWU as lane-pair kernels (bls_pp_lane.h pp2_*), fused with
 // their neighbours; they replace the wave-program phases k_h2c_iso / _pre /
@@ -538,7 +624,11 @@ static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs
     hipLaunchKernelGGL(k_g2x_pre1, g1, dim3(64), 0, st, B, status, hf, flag);
     hipLaunchKernelGGL(k_g2x_post1, g1, dim3(64), 0, st, B, status, hf, flag);
   }
-  hipLaunchKernelGGL(k_h2c_affine, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, status, hf, H);
+  if (affine_single())
+    hipLaunchKernelGGL(k_h2c_affine, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, status, hf, H);
+  else
+    hipLaunchKernelGGL(k_h2c_affine_b, dim3((unsigned)((B + 64 * AFF_K - 1) / (64 * AFF_K))), dim3(64), 0, st, B,
+                       status, hf, H);
   return hipGetLastError();
 }
 // A/B knob: BLS_H2C_VM=1 runs SSWU + the wave-program phases (k_h2c_iso / _pre / _post)
@@ -548,6 +638,8 @@ static bool h2c_use_vm() {
 }
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+
 static int env_int_or(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
@@ -578,7 +670,10 @@ static hipError_t launch_h2c_phases(hipStream_t st, size_t B, const int* status,
     if (!pass) hipLaunchKernelGGL(k_h2c_pre<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf);
   }
   hipLaunchKernelGGL(k_h2c_post<G>, dim3(nblk(B, G)), dim3(64), 0, st, B, status, hf);
-  hipLaunchKernelGGL(k_h2c_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, H);
+  if (affine_single())
+    hipLaunchKernelGGL(k_h2c_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, H);
+  else
+    hipLaunchKernelGGL(k_h2c_affine_b, dim3(nblk(B, 64 * AFF_K)), dim3(64), 0, st, B, status, hf, H);
   return hipGetLastError();
 }
 
@@ -640,7 +735,10 @@ hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status
   else
     hipLaunchKernelGGL(k_sig_vm<2>, dim3(nblk(B, 2)), dim3(64), 0, st, B, gstat, status, dstat, apk_aff, sig, rsc,
                        rPj);
-  hipLaunchKernelGGL(k_g1_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, rPj, rP);
+  if (affine_single())
+    hipLaunchKernelGGL(k_g1_affine, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, rPj, rP);
+  else
+    hipLaunchKernelGGL(k_g1_affine_b, dim3(nblk(B, 64 * AFF_K)), dim3(64), 0, st, B, status, rPj, rP);
   return hipGetLastError();
 }
 
