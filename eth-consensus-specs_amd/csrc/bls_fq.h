@@ -175,6 +175,56 @@ BLS_HD Fq fq_mul(const Fq& x, const Fq& y) {
   return r;
 }
 
+// squaring: off-diagonal digit products once, doubled with the column (v_lshl_add_u64): 105 + 14 + 196 mads
+BLS_HD Fq fq_sqr(const Fq& x) {
+  FQ_CHECK_MUL(x, x);
+  uint32_t m[14];
+  Fq r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    uint64_t od = 0;
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j > i && j < 14) od += (uint64_t)x.d[i] * x.d[j];
+    }
+#ifdef BLS_FQ_CHECK
+    unsigned __int128 chk = (unsigned __int128)acc + 2 * (unsigned __int128)od;
+#endif
+    acc += od << 1;
+    if ((k & 1) == 0 && (k >> 1) < 14) {
+      acc += (uint64_t)x.d[k >> 1] * x.d[k >> 1];
+#ifdef BLS_FQ_CHECK
+      chk += (unsigned __int128)x.d[k >> 1] * x.d[k >> 1];
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 1 && j < 14 && i < k) {
+        acc += (uint64_t)m[i] * P29[j];
+#ifdef BLS_FQ_CHECK
+        chk += (unsigned __int128)m[i] * P29[j];
+#endif
+      }
+    }
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * P29_NINV) & Q29_MASK;
+      acc += (uint64_t)m[k] * P29[0];
+#ifdef BLS_FQ_CHECK
+      chk += (unsigned __int128)m[k] * P29[0];
+#endif
+    } else {
+      r.d[k - 14] = (uint32_t)acc & Q29_MASK;
+    }
+    FQ_CHECK_COL(chk);
+    acc >>= 29;
+  }
+  r.d[13] = (uint32_t)acc;
+  return r;
+}
+
 // ---- conversions (kernel edges) -------------------------------------------
 // packed Montgomery Fp -> digits (same value, N form when the input is canonical)
 BLS_HD Fq fq_unpack(const Fp& a) {
@@ -190,5 +240,39 @@ BLS_HD Fp fq_pack(const Fq& a) {
 }
 // an N-form value (a product output, < 2p) -> canonical packed Fp without the product
 BLS_HD Fp fq_pack_n(const Fq& a) { return fp_reduce_once(fp_pack29(a.d)); }
+
+// a^e for a fixed exponent (little-endian u32 limbs, bit nbits-1 set), sliding window w = 3, every operand in N
+// form (products of products); control flow depends only on e.  Result in N form.
+BLS_HD Fq fq_pow_w3(const Fq& a, const uint32_t* e, int nbits) {
+  const Fq a2 = fq_sqr(a);
+  const Fq t1 = a;
+  const Fq t3 = fq_mul(t1, a2);
+  const Fq t5 = fq_mul(t3, a2);
+  const Fq t7 = fq_mul(t5, a2);
+  Fq r = t1;
+  bool started = false;
+  int i = nbits - 1;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      r = fq_sqr(r);
+      --i;
+      continue;
+    }
+    int j = i - 2 < 0 ? 0 : i - 2;  // window [i .. j], ending on a set bit
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) ++j;
+    uint32_t w = 0;
+    for (int k = i; k >= j; --k) w = (w << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
+    const Fq& m = w == 1u ? t1 : (w == 3u ? t3 : (w == 5u ? t5 : t7));
+    if (!started) {
+      r = m;
+      started = true;
+    } else {
+      for (int k = i; k >= j; --k) r = fq_sqr(r);
+      r = fq_mul(r, m);
+    }
+    i = j - 1;
+  }
+  return r;
+}
 
 }  // namespace bls

@@ -12,43 +12,17 @@
 // points; tests/hostcheck compares both with the oracle).
 #pragma once
 #include "bls_curve.h"
+#include "bls_fq.h"
 #include "bls_sha256.h"
 
 namespace bls {
 
-// a^e, e given as little-endian u32 limbs with bit nbits-1 set.  Control
+// a^e, e given as little-endian u32 limbs with bit nbits-1 set: sliding
+// window w = 3 in the digit form of bls_fq.h (every operand is a product
+// output, so no bound bookkeeping; ~1.4x the packed products' rate and
+// squarings at 315 instead of 390 mads), canonical packed result.  Control
 // flow depends only on e (uniform across lanes).
-BLS_HD Fp fp_pow_w3(const Fp& a, const uint32_t* e, int nbits) {
-  const Fp a2 = fp_sqr_i(a);
-  const Fp t1 = a;
-  const Fp t3 = fp_mul_i(t1, a2);
-  const Fp t5 = fp_mul_i(t3, a2);
-  const Fp t7 = fp_mul_i(t5, a2);
-  Fp r = t1;
-  bool started = false;
-  int i = nbits - 1;
-  while (i >= 0) {
-    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
-      r = fp_sqr_i(r);
-      --i;
-      continue;
-    }
-    int j = i - 2 < 0 ? 0 : i - 2;  // window [i .. j], ending on a set bit
-    while (!((e[j >> 5] >> (j & 31)) & 1u)) ++j;
-    uint32_t w = 0;
-    for (int k = i; k >= j; --k) w = (w << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
-    const Fp& m = w == 1u ? t1 : (w == 3u ? t3 : (w == 5u ? t5 : t7));
-    if (!started) {
-      r = m;
-      started = true;
-    } else {
-      for (int k = i; k >= j; --k) r = fp_sqr_i(r);
-      r = fp_mul_i(r, m);
-    }
-    i = j - 1;
-  }
-  return r;
-}
+BLS_HD Fp fp_pow_w3(const Fp& a, const uint32_t* e, int nbits) { return fq_pack_n(fq_pow_w3(fq_unpack(a), e, nbits)); }
 
 // a^(p-2): inversion with uniform control flow (no divergent GCD loop)
 BLS_HD Fp fp_inv_fermat_w3(const Fp& a) { return fp_pow_w3(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
