@@ -9,6 +9,7 @@
 //     complete (exception-free) projective formulas.
 #include "bls_kernels.h"
 #include "bls_lane.h"
+#include "bls_fq_g2.h"
 #include "bls_pp_lane.h"
 #include "bls_vm.h"
 
@@ -547,6 +548,47 @@ __device__ __forceinline__ void pp_store1(Fd* o, const PP<Fp2>& p) {
   o[5] = fd_from_fp(p.z.c1);
 }
 
+// [|x|] of a projective point through the digit-form Jacobian chain (bls_fq_g2.h): (X Z, Y Z^2, Z) in, (X Z, Y, Z^3)
+// out, canonical packed
+__device__ __forceinline__ PP<Fp2> pp_mul_xabs_q(const PP<Fp2>& P, bool& exc) {
+  const Fq2 z = fq2_unpack(P.z);
+  const J2Q J{fq2_mul(fq2_unpack(P.x), z), fq2_mul(fq2_unpack(P.y), fq2_sqr(z)), z};
+  const J2Q M = j2q_mul_xabs(J, exc);
+  return PP<Fp2>{fq2_pack(fq2_mul(M.x, M.z)), fq2_pack(M.y), fq2_pack(fq2_mul(fq2_sqr(M.z), M.z))};
+}
+static bool h2c_chain_packed() {  // A/B knob: BLS_H2C_PACKED=1 runs the cofactor chains on packed Fp (j2_*)
+  static const bool packed = getenv("BLS_H2C_PACKED") != nullptr;
+  return packed;
+}
+
+template <bool DIGITS>
+__global__ void __launch_bounds__(64) k_g2x_pre1t(size_t B, const int* status, Fd* hf, int* flag) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || (status && !status[i])) return;
+  Fd* r = hf + HCF * i;
+  const PP<Fp2> Q = pp2_load(r + HCF_Q);
+  bool exc = false;
+  const PP<Fp2> M = DIGITS ? pp_mul_xabs_q(Q, exc) : j2_to_pp(j2_mul_xabs(j2_from_pp(Q), exc));
+  const PP<Fp2> pq = pp_psi2x(Q);
+  pp_store1(r + HCF_A, pp_add(pq, pp_neg2(M)));  // t1 + t2, t1 = -M
+  const PP<Fp2> mq = pp_add(M, pp_neg2(Q));
+  const PP<Fp2> t3{f2mul(Q.x, PSI2_CX), f2mul(Q.y, PSI2_CY), Q.z};  // psi^2(Q); psi^2(2Q) = 2 psi^2(Q)
+  pp_store1(r + HCF_C, pp_add(pp_add(pp_dbl(t3), pp_neg2(pq)), mq));
+  if (exc) flag[i] = 1;
+}
+
+template <bool DIGITS>
+__global__ void __launch_bounds__(64) k_g2x_post1t(size_t B, const int* status, Fd* hf, int* flag) {
+  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= B || (status && !status[i])) return;
+  Fd* r = hf + HCF * i;
+  bool exc = false;
+  const PP<Fp2> A = pp2_load(r + HCF_A);
+  const PP<Fp2> M = DIGITS ? pp_mul_xabs_q(A, exc) : j2_to_pp(j2_mul_xabs(j2_from_pp(A), exc));
+  pp_store1(r + HCF_A, pp_add(pp2_load(r + HCF_C), pp_neg2(M)));  // projective H over the dead A slots
+  if (exc) flag[i] = 1;
+}
+
 __global__ void __launch_bounds__(64) k_g2x_pre1(size_t B, const int* status, Fd* hf, int* flag) {
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B || (status && !status[i])) return;
@@ -620,9 +662,12 @@ static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs
   } else if (pair_chains) {
     hipLaunchKernelGGL(k_g2x_pre2, g, dim3(64), 0, st, B, hf);
     hipLaunchKernelGGL(k_g2x_post2, g, dim3(64), 0, st, B, hf);
+  } else if (h2c_chain_packed()) {
+    hipLaunchKernelGGL(k_g2x_pre1t<false>, g1, dim3(64), 0, st, B, status, hf, flag);
+    hipLaunchKernelGGL(k_g2x_post1t<false>, g1, dim3(64), 0, st, B, status, hf, flag);
   } else {
-    hipLaunchKernelGGL(k_g2x_pre1, g1, dim3(64), 0, st, B, status, hf, flag);
-    hipLaunchKernelGGL(k_g2x_post1, g1, dim3(64), 0, st, B, status, hf, flag);
+    hipLaunchKernelGGL(k_g2x_pre1t<true>, g1, dim3(64), 0, st, B, status, hf, flag);
+    hipLaunchKernelGGL(k_g2x_post1t<true>, g1, dim3(64), 0, st, B, status, hf, flag);
   }
   if (affine_single())
     hipLaunchKernelGGL(k_h2c_affine, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, B, status, hf, H);

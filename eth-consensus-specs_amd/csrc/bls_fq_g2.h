@@ -1,0 +1,99 @@
+// Fp2 products and the Jacobian [|x|] chain of the cofactor clearing in the
+// redundant digit form of bls_fq.h.
+//
+// Every stored value is in L form (carry-save normalised digits); the
+// subtraction constant of each step is the smallest multiple of p (64p ..
+// 2048p, bls_fq_constants.h) that covers its subtrahend's digits and value,
+// and every product's operand values stay far enough below p R (R / p ~ 2^25.3)
+// -- the bounds written beside each step are in units of p, for the chain's
+// state X < 1030p, Y < 650p, Z < 270p.  The host tests
+// (tests/test_hostcheck.py::test_fq_g2_chain) run the whole chain with the
+// 128-bit column, value and subtraction checks of bls_fq.h compiled in.
+#pragma once
+#include "bls_fq.h"
+#include "bls_tower.h"
+
+namespace bls {
+
+template <const uint32_t* K>
+BLS_HD Fq fq_subk(const Fq& a, const Fq& b) {
+  FQ_CHECK_SUB(b, K);
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = a.d[i] + (K[i] - b.d[i]);
+  return r;
+}
+template <const uint32_t* K>
+BLS_HD Fq2 fq2_subk(const Fq2& a, const Fq2& b) {
+  return Fq2{fq_subk<K>(a.c0, b.c0), fq_subk<K>(a.c1, b.c1)};
+}
+BLS_HD Fq2 fq2_add(const Fq2& a, const Fq2& b) { return Fq2{fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)}; }
+BLS_HD Fq2 fq2_norm(const Fq2& a) { return Fq2{fq_norm(a.c0), fq_norm(a.c1)}; }
+BLS_HD Fq2 fq2_mul_small(const Fq2& a, uint32_t k) { return Fq2{fq_mul_small(a.c0, k), fq_mul_small(a.c1, k)}; }
+
+// Karatsuba, operands in L form: c0 = t0 - t1 + 64p (< 66p), c1 = t2 - t0 - t1 + 128p (< 130p), both normalised
+BLS_HD Fq2 fq2_mul(const Fq2& a, const Fq2& b) {
+  const Fq t0 = fq_mul(a.c0, b.c0), t1 = fq_mul(a.c1, b.c1);
+  const Fq t2 = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
+  return Fq2{fq_norm(fq_subk<Q29_K1>(t0, t1)), fq_norm(fq_subk<Q29_K2>(t2, fq_add(t0, t1)))};
+}
+// (a0 + a1)(a0 - a1), 2 a0 a1 for a in L form with a1 < 2046p: c0 < 2p, c1 < 4p
+BLS_HD Fq2 fq2_sqr(const Fq2& a) {
+  const Fq t0 = fq_mul(fq_add(a.c0, a.c1), fq_norm(fq_subk<Q29_K2048_2>(a.c0, a.c1)));
+  const Fq t1 = fq_mul(a.c0, a.c1);
+  return Fq2{t0, fq_mul_small(t1, 2)};
+}
+BLS_HD Fq2 fq2_unpack(const Fp2& a) { return Fq2{fq_unpack(a.c0), fq_unpack(a.c1)}; }
+BLS_HD Fp2 fq2_pack(const Fq2& a) { return Fp2{fq_pack(a.c0), fq_pack(a.c1)}; }
+
+struct J2Q {
+  Fq2 x, y, z;
+};
+
+// dbl-2009-l: X < 1030p, Y < 650p, Z < 270p in -> X3 < 1028p, Y3 < 194p, Z3 < 260p
+BLS_HD J2Q j2q_dbl(const J2Q& p) {
+  const Fq2 A = fq2_sqr(p.x);                                      // (2, 4)
+  const Fq2 Bq = fq2_sqr(p.y);
+  const Fq2 C = fq2_sqr(Bq);
+  const Fq2 XB2 = fq2_sqr(fq2_norm(fq2_add(p.x, Bq)));
+  const Fq2 D = fq2_mul_small(fq2_subk<Q29_K2>(XB2, fq2_add(A, C)), 2);  // 2 (XB2 - A - C + 128p) < 264p
+  const Fq2 E = fq2_mul_small(A, 3);                               // < 12p
+  J2Q r;
+  r.x = fq2_norm(fq2_subk<Q29_K1024>(fq2_sqr(E), fq2_mul_small(D, 2)));  // F - 2D + 1024p < 1028p
+  const Fq2 DX = fq2_norm(fq2_subk<Q29_K2048_2>(D, r.x));         // < 2312p
+  r.y = fq2_norm(fq2_subk<Q29_K1>(fq2_mul(E, DX), fq2_mul_small(C, 8)));  // < 194p
+  r.z = fq2_mul_small(fq2_mul(p.y, p.z), 2);                       // < 260p
+  return r;
+}
+
+// add-2007-bl (incomplete): exc |= the exceptional cases (h = 0, an identity operand), checked on canonical values
+BLS_HD J2Q j2q_add(const J2Q& p, const J2Q& q, bool& exc) {
+  const Fq2 z1z1 = fq2_sqr(p.z), z2z2 = fq2_sqr(q.z);
+  const Fq2 u1 = fq2_mul(p.x, z2z2), u2 = fq2_mul(q.x, z1z1);        // (66, 130)
+  const Fq2 s1 = fq2_mul(fq2_mul(p.y, q.z), z2z2), s2 = fq2_mul(fq2_mul(q.y, p.z), z1z1);
+  const Fq2 h = fq2_norm(fq2_subk<Q29_K256>(u2, u1));              // < 386p
+  exc = exc || fp2_is_zero(fq2_pack(h)) || fp2_is_zero(fq2_pack(p.z)) || fp2_is_zero(fq2_pack(q.z));
+  const Fq2 rr = fq2_mul_small(fq2_subk<Q29_K256>(s2, s1), 2);     // < 772p
+  const Fq2 i = fq2_sqr(fq2_mul_small(h, 2));
+  const Fq2 j = fq2_mul(h, i), v = fq2_mul(u1, i);
+  J2Q r;
+  r.x = fq2_norm(fq2_subk<Q29_K512_2>(fq2_sqr(rr), fq2_add(j, fq2_mul_small(v, 2))));  // < 516p
+  const Fq2 vx = fq2_norm(fq2_subk<Q29_K1024>(v, r.x));           // < 1154p
+  r.y = fq2_norm(fq2_subk<Q29_K512_2>(fq2_mul(rr, vx), fq2_mul_small(fq2_mul(s1, j), 2)));  // < 642p
+  const Fq2 zz = fq2_norm(fq2_subk<Q29_K2>(fq2_sqr(fq2_norm(fq2_add(p.z, q.z))), fq2_add(z1z1, z2z2)));
+  r.z = fq2_mul(zz, h);                                              // (66, 130)
+  return r;
+}
+
+// [|x|] p (the leading bit of |x| is bit 63)
+BLS_HD J2Q j2q_mul_xabs(const J2Q& p, bool& exc) {
+  J2Q m = p;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    m = j2q_dbl(m);
+    if ((X_ABS >> b) & 1ull) m = j2q_add(m, p, exc);
+  }
+  return m;
+}
+
+}  // namespace bls

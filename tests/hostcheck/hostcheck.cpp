@@ -9,6 +9,7 @@
 #include "bls_tower_inline.h"
 #include "bls_pp_lane.h"
 #include "bls_fq_g1.h"
+#include "bls_fq_g2.h"
 #include <string.h>
 using namespace bls;
 
@@ -184,4 +185,18 @@ extern "C" void hc_fq_g1_mul64(const uint8_t* p, uint64_t r, uint8_t* o) {
   const Fp zi = fp_inv(Z);
   out_fp(o, fp_mul(X, zi));
   out_fp(o + 48, fp_mul(Y, zi));
+}
+
+// [|x|] q through the digit-form Jacobian chain of the hash_to_G2 kernels (bls_fq_g2.h), q affine in, affine out;
+// returns the exception flag
+extern "C" int hc_fq_j2_mul_xabs(const uint8_t* q, uint8_t* o) {
+  const Fq2 z = fq2_unpack(fp2_one());
+  const J2Q J{fq2_mul(fq2_unpack(in_fp2(q)), z), fq2_mul(fq2_unpack(in_fp2(q + 96)), fq2_sqr(z)), z};
+  bool exc = false;
+  const J2Q M = j2q_mul_xabs(J, exc);
+  const Fp2 X = fq2_pack(fq2_mul(M.x, M.z)), Y = fq2_pack(M.y), Z = fq2_pack(fq2_mul(fq2_sqr(M.z), M.z));
+  const Fp2 zi = fp2_inv(Z);
+  out_fp2(o, fp2_mul(X, zi));
+  out_fp2(o + 96, fp2_mul(Y, zi));
+  return exc ? 1 : 0;
 }

@@ -313,3 +313,14 @@ def test_fq_g1_scalar_chain():
         out = H.call("hc_fq_g1_mul64", H.fp_b(p[0]) + H.fp_b(p[1]), r, out=96)
         want = O.g1_mul(p, r)
         assert (H.b_fp(out[:48]), H.b_fp(out[48:])) == (want[0], want[1])
+
+
+def test_fq_g2_chain():
+    """The cofactor chain [|x|] Q in the digit form (bls_fq_g2.h j2q_*) with the 128-bit column, value and
+    subtraction checks compiled in, against the oracle, on points of G2 and on points of E2 outside G2 (the
+    chain's inputs are not in G2)."""
+    pts = [O.g2_mul(O.G2_GEN, rng.randrange(1, O.R)) for _ in range(4)]
+    pts += [O.iso_map(O.map_to_curve_sswu(rfp2())) for _ in range(4)]
+    for q in pts:
+        exc, out = H.call("hc_fq_j2_mul_xabs", H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192, ret=True)
+        assert exc == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.g2_mul(q, O.X_ABS)
