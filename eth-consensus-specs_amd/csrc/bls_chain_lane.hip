@@ -10,6 +10,7 @@
 //   k_g2x_lane   M = [|x|] B on the hash_to_G2 staging slots (cofactor clearing)
 #include "bls_kernels.h"
 #include "bls_fq_g1.h"
+#include "bls_fq_g2.h"
 #include "bls_pp_lane.h"
 #include "bls_vm.h"
 
@@ -219,13 +220,68 @@ __global__ void __launch_bounds__(64) k_sig_lane1j(size_t B, const int* gstat, i
   status[i] = ok ? 1 : 0;
 }
 
+// k_sig_lane1j with both chains in the digit form (bls_fq_g1.h, bls_fq_g2.h): one lane per chain, the G2 chain
+// Jacobian with flagged exceptional additions (those items rerun the complete projective chain).
+__global__ void __launch_bounds__(64) k_sig_lane1q(size_t B, const int* gstat, int* status, const int* dstat,
+                                                   const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
+  const unsigned nb = (unsigned)((B + 63) / 64);
+  const bool g2 = blockIdx.x >= nb;
+  const size_t i = (size_t)(g2 ? blockIdx.x - nb : blockIdx.x) * 64 + threadIdx.x;
+  if (i >= B) return;
+  const bool live = gstat[i] && dstat[i];
+  if (!g2) {
+    if (!live) return;
+    const G1P a = apk[i];
+    const G1Q A{fq_unpack(a.x), fq_unpack(a.y), fq_unpack(a.z)};
+    const uint64_t r = rsc[i];
+    G1Q R{fq_zero(), fq_unpack(FP_ONE), fq_zero()};
+    if ((r >> 63) & 1ull) R = A;
+#pragma unroll 1
+    for (int b = 62; b >= 0; --b) {
+      R = g1q_dbl(R);
+      if ((r >> b) & 1ull) R = g1q_add(R, A);
+    }
+    rPj[i] = G1P{fq_pack(R.x), fq_pack(R.y), fq_pack(R.z)};
+    return;
+  }
+  if (!live) {
+    status[i] = 0;
+    return;
+  }
+  const G2A s = sig[i];
+  bool exc = false;
+  const J2Q M = j2q_mul_xabs(J2Q{fq2_unpack(s.x), fq2_unpack(s.y), fq2_unpack(fp2_one())}, exc);
+  const Fp2 px = f2mul(fp2_conj(s.x), PSI_CX), py = f2mul(fp2_conj(s.y), PSI_CY);
+  bool ok;
+  if (!exc) {  // psi(sigma) == -M:  px Z^2 == X, py Z^3 == -Y, Z != 0
+    const Fp2 X = fq2_pack(M.x), Y = fq2_pack(M.y), Z = fq2_pack(M.z);
+    const Fp2 zz = f2sqr(Z);
+    ok = fp2_is_zero(fp2_sub(f2mul(px, zz), X)) && fp2_is_zero(fp2_add(f2mul(py, f2mul(zz, Z)), Y)) &&
+         !fp2_is_zero(Z);
+  } else {  // complete formulas (k_sig_lane)
+    PP<Fp2> P{s.x, s.y, fp2_one()};
+#pragma unroll 1
+    for (int b = 62; b >= 0; --b) {
+      P = pp_dbl(P);
+      if ((X_ABS >> b) & 1ull) P = pp_add_aff(P, s.x, s.y);
+    }
+    ok = fp2_is_zero(fp2_sub(f2mul(px, P.z), P.x)) && fp2_is_zero(fp2_add(f2mul(py, P.z), P.y)) &&
+         !fp2_is_zero(P.z);
+  }
+  status[i] = ok ? 1 : 0;
+}
+
 hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
                            const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   if (!B) return hipSuccess;
   // A/B knobs: BLS_SIG1 = k_sig_lane (one lane per G2 chain, complete formulas), BLS_SIG1J = k_sig_lane1j (one
   // lane, Jacobian; 1.41-1.43M FAV/s against 1.43-1.50M for the lane pairs: its 512 registers still spill)
   static const bool one_lane = getenv("BLS_SIG1") != nullptr, jac = getenv("BLS_SIG1J") != nullptr;
-  if (jac)
+  static const bool digits = getenv("BLS_SIG1Q") != nullptr;  // A/B knob: k_sig_lane1q (digit-form chains)
+  if (digits)
+    hipLaunchKernelGGL(k_sig_lane1q, dim3(2 * (unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat,
+                       apk, sig, rsc, rPj);
+  else if (jac)
     hipLaunchKernelGGL(k_sig_lane1j, dim3(2 * (unsigned)((B + 63) / 64)), dim3(64), 0, st, B, gstat, status, dstat,
                        apk, sig, rsc, rPj);
   else if (one_lane)
