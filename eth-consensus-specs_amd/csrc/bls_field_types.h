@@ -9,7 +9,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef BLS_HD  // the host test harness's digit-form unit (tests/hostcheck/hostcheck_fq.cpp) predefines it without
+                // the forced inlining: its checked products inlined everywhere took ~15 min to compile
 #define BLS_HD __host__ __device__ __forceinline__
+#endif
 #define BLS_HDNI __host__ __device__ inline __attribute__((noinline))
 
 namespace bls {

@@ -3,13 +3,10 @@
 // container without a GPU.  Never linked into libblsmi355x.so, never loaded
 // by the product shim.  All values cross the boundary as canonical
 // big-endian integers (48 bytes per Fp).
-#define BLS_FQ_CHECK 1  // 128-bit column and precondition checks of the digit form (bls_fq.h)
 #include "bls_ops.h"
 #include "bls_lane.h"
 #include "bls_tower_inline.h"
 #include "bls_pp_lane.h"
-#include "bls_fq_g1.h"
-#include "bls_fq_g2.h"
 #include <string.h>
 using namespace bls;
 
@@ -136,67 +133,3 @@ extern "C" int hc_j2_add_aff(const uint8_t* p, const uint8_t* q, uint8_t* o) {
   return exc ? 1 : 0;
 }
 
-// registry-gather formulas in the digit form (bls_fq_g1.h): pts = n affine points (x || y, 96 B each), the first
-// `split` summed into one accumulator and the rest into another by g1q_add_aff, then g1q_add; out = affine sum
-// (x || y) or 96 zero bytes for the identity
-extern "C" void hc_fq_gather(const uint8_t* pts, uint32_t n, uint32_t split, uint8_t* o) {
-  const G1Q id{fq_zero(), fq_unpack(FP_ONE), fq_zero()};
-  G1Q a = id, b = id;
-  for (uint32_t k = 0; k < n; ++k) {
-    const Fq x = fq_unpack(in_fp(pts + 96 * k)), y = fq_unpack(in_fp(pts + 96 * k + 48));
-    if (k < split)
-      a = g1q_add_aff(a, x, y);
-    else
-      b = g1q_add_aff(b, x, y);
-  }
-  const G1Q s = g1q_add(a, b);
-  const Fp X = fq_pack(s.x), Y = fq_pack(s.y), Z = fq_pack(s.z);
-  if (fp_is_zero(Z)) {
-    memset(o, 0, 96);
-    return;
-  }
-  const Fp zi = fp_inv(Z);
-  out_fp(o, fp_mul(X, zi));
-  out_fp(o + 48, fp_mul(Y, zi));
-}
-// one digit-form product of raw digit vectors (14 x u32 each): r = x y / 2^406, digits
-extern "C" void hc_fq_mul_digits(const uint32_t* x, const uint32_t* y, uint32_t* r) {
-  Fq a, b;
-  memcpy(a.d, x, 56);
-  memcpy(b.d, y, 56);
-  const Fq c = fq_mul(a, b);
-  memcpy(r, c.d, 56);
-}
-
-// r * P by the digit-form double-and-add of k_sig_lane2 (bls_fq_g1.h g1q_dbl / g1q_add), 64-bit r; out affine
-extern "C" void hc_fq_g1_mul64(const uint8_t* p, uint64_t r, uint8_t* o) {
-  const G1Q A{fq_unpack(in_fp(p)), fq_unpack(in_fp(p + 48)), fq_unpack(FP_ONE)};
-  G1Q R{fq_zero(), fq_unpack(FP_ONE), fq_zero()};
-  if ((r >> 63) & 1ull) R = A;
-  for (int b = 62; b >= 0; --b) {
-    R = g1q_dbl(R);
-    if ((r >> b) & 1ull) R = g1q_add(R, A);
-  }
-  const Fp X = fq_pack(R.x), Y = fq_pack(R.y), Z = fq_pack(R.z);
-  if (fp_is_zero(Z)) {
-    memset(o, 0, 96);
-    return;
-  }
-  const Fp zi = fp_inv(Z);
-  out_fp(o, fp_mul(X, zi));
-  out_fp(o + 48, fp_mul(Y, zi));
-}
-
-// [|x|] q through the digit-form Jacobian chain of the hash_to_G2 kernels (bls_fq_g2.h), q affine in, affine out;
-// returns the exception flag
-extern "C" int hc_fq_j2_mul_xabs(const uint8_t* q, uint8_t* o) {
-  const Fq2 z = fq2_unpack(fp2_one());
-  const J2Q J{fq2_mul(fq2_unpack(in_fp2(q)), z), fq2_mul(fq2_unpack(in_fp2(q + 96)), fq2_sqr(z)), z};
-  bool exc = false;
-  const J2Q M = j2q_mul_xabs(J, exc);
-  const Fp2 X = fq2_pack(fq2_mul(M.x, M.z)), Y = fq2_pack(M.y), Z = fq2_pack(fq2_mul(fq2_sqr(M.z), M.z));
-  const Fp2 zi = fp2_inv(Z);
-  out_fp2(o, fp2_mul(X, zi));
-  out_fp2(o + 96, fp2_mul(Y, zi));
-  return exc ? 1 : 0;
-}

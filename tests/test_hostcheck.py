@@ -324,3 +324,17 @@ def test_fq_g2_chain():
     for q in pts:
         exc, out = H.call("hc_fq_j2_mul_xabs", H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192, ret=True)
         assert exc == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.g2_mul(q, O.X_ABS)
+
+
+def test_fq_g2_add_exception():
+    """j2q_add (digit form): 2p + q matches the oracle; q = -2p (h = 0) raises the exception flag that routes an
+    item to the hash_to_G2 fallback."""
+    p = O.g2_mul(O.G2_GEN, 11)
+    for q in (O.g2_mul(O.G2_GEN, 5), O.iso_map(O.map_to_curve_sswu(rfp2()))):
+        exc, out = H.call("hc_fq_j2_dbl_add", H.fp2_b(p[0]) + H.fp2_b(p[1]), H.fp2_b(q[0]) + H.fp2_b(q[1]),
+                          out=192, ret=True)
+        assert exc == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.g2_add(O.g2_mul(p, 2), q)
+    q = O.g2_neg(O.g2_mul(p, 2))
+    exc, _ = H.call("hc_fq_j2_dbl_add", H.fp2_b(p[0]) + H.fp2_b(p[1]), H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192,
+                    ret=True)
+    assert exc == 1
