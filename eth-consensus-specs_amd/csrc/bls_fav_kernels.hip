@@ -550,7 +550,9 @@ __device__ __forceinline__ void pp_store1(Fd* o, const PP<Fp2>& p) {
 
 // [|x|] of a projective point through the digit-form Jacobian chain (bls_fq_g2.h): (X Z, Y Z^2, Z) in, (X Z, Y, Z^3)
 // out, canonical packed
-__device__ __forceinline__ PP<Fp2> pp_mul_xabs_q(const PP<Fp2>& P, bool& exc) {
+// (noinline: one copy for both kernels; a call per chain is nothing against its 68 steps, and inlined twice it
+// doubled this file's device compile time)
+__device__ __noinline__ PP<Fp2> pp_mul_xabs_q(const PP<Fp2>& P, bool& exc) {
   const Fq2 z = fq2_unpack(P.z);
   const J2Q J{fq2_mul(fq2_unpack(P.x), z), fq2_mul(fq2_unpack(P.y), fq2_sqr(z)), z};
   const J2Q M = j2q_mul_xabs(J, exc);
@@ -589,30 +591,6 @@ __global__ void __launch_bounds__(64) k_g2x_post1t(size_t B, const int* status, 
   if (exc) flag[i] = 1;
 }
 
-__global__ void __launch_bounds__(64) k_g2x_pre1(size_t B, const int* status, Fd* hf, int* flag) {
-  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= B || (status && !status[i])) return;
-  Fd* r = hf + HCF * i;
-  const PP<Fp2> Q = pp2_load(r + HCF_Q);
-  bool exc = false;
-  const PP<Fp2> M = j2_to_pp(j2_mul_xabs(j2_from_pp(Q), exc));
-  const PP<Fp2> pq = pp_psi2x(Q);
-  pp_store1(r + HCF_A, pp_add(pq, pp_neg2(M)));  // t1 + t2, t1 = -M
-  const PP<Fp2> mq = pp_add(M, pp_neg2(Q));
-  const PP<Fp2> t3{f2mul(Q.x, PSI2_CX), f2mul(Q.y, PSI2_CY), Q.z};  // psi^2(Q); psi^2(2Q) = 2 psi^2(Q)
-  pp_store1(r + HCF_C, pp_add(pp_add(pp_dbl(t3), pp_neg2(pq)), mq));
-  if (exc) flag[i] = 1;
-}
-
-__global__ void __launch_bounds__(64) k_g2x_post1(size_t B, const int* status, Fd* hf, int* flag) {
-  const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= B || (status && !status[i])) return;
-  Fd* r = hf + HCF * i;
-  bool exc = false;
-  const PP<Fp2> M = j2_to_pp(j2_mul_xabs(j2_from_pp(pp2_load(r + HCF_A)), exc));
-  pp_store1(r + HCF_A, pp_add(pp2_load(r + HCF_C), pp_neg2(M)));  // projective H over the dead A slots
-  if (exc) flag[i] = 1;
-}
 
 // The same split into lean kernels: the one-lane Jacobian chain alone (its
 // register budget is the chain's), and the pre/post steps on lane pairs.
@@ -649,7 +627,7 @@ static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs
                                    const int* status, Fd* hf, G2A* H, int* flag) {
   const dim3 g((unsigned)((2 * B + 63) / 64));
   hipLaunchKernelGGL(k_h2c_sswu_iso2, g, dim3(64), 0, st, B, msgs, offs, status, hf, flag);
-  // default: one-lane Jacobian chains fused with pre/post (k_g2x_pre1 / _post1).  A/B knobs (interleaved medians,
+  // default: one-lane Jacobian chains fused with pre/post (k_g2x_pre1t / _post1t, digit form).  A/B knobs (interleaved medians,
   // profiles/r02o_h2c_chains_ab.txt): BLS_H2C_SPLIT = one-lane chains alone + lane-pair pre/post kernels (1.465M
   // FAV/s against 1.482M), BLS_H2C_CHAIN2 = lane-pair complete-formula chains fused with pre/post (1.437M)
   static const bool pair_chains = getenv("BLS_H2C_CHAIN2") != nullptr, split = getenv("BLS_H2C_SPLIT") != nullptr;
