@@ -1,21 +1,41 @@
 #!/usr/bin/env python3
 """bench.py -- FastAggregateVerify throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): sync-committee
-FastAggregateVerify, 10,000 aggregates x 512 pubkeys per GPU, pubkeys named
-by index into a 2^20-key registry resident in HBM (sk_i = i + 1), distinct
-32-byte messages SHA256(seed||rank||j), valid aggregate signatures made on
-the device.  One step = one pass of the hot path over the batch: registry
-gather + aggregate pubkeys, signature decode/subgroup checks, hash_to_G2,
-random-linear-combination Miller loops, one shared final exponentiation
-(per-item fallback only on failure), verdicts written to HBM.
+Headline workload (--config c2, the default; BASELINE.json configs[1], SURVEY.md
+§8(d) C2): sync-committee FastAggregateVerify, 10,000 aggregates x 512 pubkeys
+per GPU, pubkeys named by index into a 2^20-key registry resident in HBM
+(sk_i = i + 1), distinct 32-byte messages SHA256(seed||rank||j), valid
+aggregate signatures made on the device.  One step = one pass of the hot path
+over the batch: registry gather + aggregate pubkeys, signature decode/subgroup
+checks, hash_to_G2, random-linear-combination Miller loops, one shared final
+exponentiation (per-item fallback only on failure), verdicts written to HBM.
+
+The other BASELINE configs are selectable (the driver runs c2; every config
+runs at any world size through the same RCCL exchange):
+  --config c3  mainnet epoch replay (configs[2]): a seeded permutation of the
+               2^20 registry, 32 slots x 64 committees of 512 = 2,048 FAV per
+               epoch; the epoch is sharded over the ranks (strong scaling), each
+               rank's Miller partial all-gathered over RCCL, one verdict per
+               epoch.  One step = one epoch.
+  --config c4  gossip firehose (configs[3]): 10^6 single-signature Verify with
+               distinct messages, contiguous shards of 10^6 / world (125,000 at
+               8 GPUs), each shard in 125,000-item jobs.  One step = 10^6 Verify.
+  --config c5  adversarial FAV batches (configs[4]): 1,024 x 512 per rank with
+               k bad items of every SURVEY §8(d) kind (bisection fallback each
+               step), plus AggregateVerify with N = 128 .. 8,192 distinct
+               messages as secondary figures.
+The c2 line also carries a C3 epoch-replay figure (`c3`) and, on rank 0, a
+parity sample (`parity`): an adversarial 1,024 x 512 slice with 8 bad items of
+each kind checked against the construction and, on 16 sampled items, against
+the C oracle; hash_to_G2 of the golden messages against their committed
+points; the deposit-cli known answer through the per-call API.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py
---gpus N): weak scaling, each rank owns its own batch; the ranks' 576-byte
-Fp12 Miller partials are all-gathered by the library over RCCL
-(bls_fav_job_check_comm: ncclAllGather on the device, xGMI) and every rank
-final-exponentiates the product.  torch.distributed (gloo) is only the
-control plane: rendezvous, the RCCL unique id, barriers, max over ranks.
+--gpus N): the ranks' 576-byte Fp12 Miller partials are all-gathered by the
+library over RCCL (bls_fav_job_check_comm: ncclAllGather on the device, xGMI)
+and every rank final-exponentiates the product.  torch.distributed (gloo) is
+only the control plane: rendezvous, the RCCL unique id, barriers, max over
+ranks.
 
 Roofline: after the timed region, a few passes run one batch at a time with
 per-kernel hipEvent timing (bls_profile_*), so each kernel's average is its
@@ -58,6 +78,15 @@ GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x,
 # profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
 KERNEL_SYMBOL = {"miller": "k_miller_acc4<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
+LIB = os.path.join(ROOT, "eth-consensus-specs_amd", "libblsmi355x.so")
+
+REG_N = 1 << 20
+G1_INF = b"\xc0" + bytes(47)
+PK_0x40 = b"\x40" + bytes(47)
+IDX_INF, IDX_0x40 = REG_N, REG_N + 1  # invalid keys appended after the 2^20 generated ones
+BAD_KINDS = ("wrong_msg", "inf_sig", "zero_sig", "ff_tail", "g1_inf_pk", "pk_0x40")
+C3_SLOTS, C3_PER_SLOT, C3_N = 32, 64, 512  # presets/mainnet/phase0.yaml: SLOTS_PER_EPOCH, MAX_COMMITTEES_PER_SLOT
+C4_TOTAL, C4_CHUNK = 10 ** 6, 125_000
 
 
 def model_fme(n: int):
@@ -75,8 +104,33 @@ def model_fme(n: int):
     }
 
 
+def item_ops(n: int) -> int:
+    """SURVEY.md §8(d) int ops of one registry-resident FAV(n) (Verify: n = 1)."""
+    return (11 * (n - 1) + 14789) * FME_OPS + 19 * SHA_OPS
+
+
+BATCH_OPS = 9268 * FME_OPS  # shared per batch: 63 Fp12 squarings x 36 + final exponentiation (§8(d))
+
+
+# ------------------------------------------------------------------ workloads --
+def shard_bounds(total: int, rank: int, world: int) -> tuple[int, int]:
+    base, extra = divmod(total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def _msg(tag: bytes, seed: int, j: int) -> bytes:
+    return hashlib.sha256(tag + seed.to_bytes(8, "little") + int(j).to_bytes(8, "little")).digest()
+
+
+def _agg_sks(idx2d: np.ndarray) -> bytes:
+    """Aggregate secret key of each committee (sk_i = i + 1; the sum stays far below r)."""
+    agg = (idx2d.astype(np.int64) + 1).sum(axis=1)
+    return b"".join(int(a).to_bytes(32, "big") for a in agg)
+
+
 def build_inputs(B: int, n: int, reg_n: int, seed: int, rank: int):
-    """Committees, messages and aggregate secret keys (host, numpy)."""
+    """C2: B committees of n distinct indices, messages and aggregate secret keys (host, numpy)."""
     rng = np.random.default_rng(seed * 1000003 + rank)
     total = B * n
     perms = []
@@ -85,13 +139,76 @@ def build_inputs(B: int, n: int, reg_n: int, seed: int, rank: int):
     idx = np.concatenate(perms)[:total] if len(perms) > 1 else perms[0][:total]
     assert reg_n % n == 0  # committees never straddle two permutations: indices distinct per committee
     offs = np.arange(B + 1, dtype=np.uint64) * n
-    agg = (idx.reshape(B, n).astype(np.int64) + 1).sum(axis=1)  # < r, fits int64
-    sks = b"".join(int(a).to_bytes(32, "big") for a in agg)
     msgs = b"".join(hashlib.sha256(b"bench" + seed.to_bytes(8, "little") + rank.to_bytes(4, "little")
                                    + j.to_bytes(8, "little")).digest() for j in range(B))
-    return idx, offs, msgs, sks
+    return idx, offs, msgs, _agg_sks(idx.reshape(B, n))
 
 
+def c3_shard(reg_n: int, seed: int, rank: int, world: int):
+    """C3: this rank's contiguous block of the epoch's 2,048 committees (a seeded permutation of the registry
+    split into 32 slots x 64 committees of 512; one message per (slot, committee)).  Every rank draws the same
+    permutation, so the shards partition the epoch."""
+    B = C3_SLOTS * C3_PER_SLOT
+    n = C3_N
+    assert B * n <= reg_n
+    perm = np.random.default_rng(seed).permutation(reg_n).astype(np.uint32)[: B * n].reshape(B, n)
+    lo, hi = shard_bounds(B, rank, world)
+    idx2d = perm[lo:hi]
+    msgs = b"".join(_msg(b"epoch", seed, j) for j in range(lo, hi))
+    return idx2d.reshape(-1), np.arange(hi - lo + 1, dtype=np.uint64) * n, msgs, _agg_sks(idx2d), (lo, hi)
+
+
+def c4_shard(total: int, seed: int, rank: int, world: int, chunk: int = C4_CHUNK):
+    """C4: Verify i (i < total) with pk_i = registry[i], m_i distinct, sk_i = i + 1; this rank's contiguous
+    shard, run as jobs of `chunk` items (one job when the shard does not split evenly)."""
+    lo, hi = shard_bounds(total, rank, world)
+    B = hi - lo
+    idx = np.arange(lo, hi, dtype=np.uint32)
+    msgs = b"".join(_msg(b"gossip", seed, j) for j in range(lo, hi))
+    sks = b"".join(int(i + 1).to_bytes(32, "big") for i in range(lo, hi))
+    chunks = B // chunk if chunk and B % chunk == 0 and B >= chunk else 1
+    return idx, np.arange(B + 1, dtype=np.uint64), msgs, sks, chunks, (lo, hi)
+
+
+def corrupt(sigs: bytearray, idx2d: np.ndarray, j: int, kind: str, B: int) -> None:
+    """Make item j invalid in one of the SURVEY.md §8(d) ways (test_eth_fast_aggregate_verify.py:38-151 cases)."""
+    if kind == "wrong_msg":  # a valid G2 point for another message: only the pairing check catches it
+        o = (j + 1) % B
+        sigs[96 * j: 96 * j + 96] = sigs[96 * o: 96 * o + 96]
+    elif kind == "inf_sig":
+        sigs[96 * j: 96 * j + 96] = b"\xc0" + bytes(95)
+    elif kind == "zero_sig":
+        sigs[96 * j: 96 * j + 96] = bytes(96)
+    elif kind == "ff_tail":  # test_eth_fast_aggregate_verify.py:104
+        sigs[96 * j + 92: 96 * j + 96] = b"\xff" * 4
+    elif kind == "g1_inf_pk":
+        idx2d[j, 7] = IDX_INF
+    elif kind == "pk_0x40":
+        idx2d[j, 0] = IDX_0x40
+    else:
+        raise ValueError(kind)
+
+
+def adversarial_plan(B: int, per_kind: int, seed: int) -> dict:
+    """Seeded positions: per_kind distinct items for each bad kind."""
+    rng = np.random.default_rng(seed)
+    pos = rng.choice(B, size=per_kind * len(BAD_KINDS), replace=False)
+    return {int(j): BAD_KINDS[t // per_kind] for t, j in enumerate(pos)}
+
+
+def adversarial_inputs(batch, ctx, B: int, n: int, plan: dict, seed: int, reg_n: int = REG_N):
+    rng = np.random.default_rng(seed)
+    idx2d = np.stack([rng.choice(reg_n, size=n, replace=False) for _ in range(B)]).astype(np.uint32)
+    msgs = [_msg(b"adv", seed, j) for j in range(B)]
+    sigs = bytearray(batch.sign_batch(_agg_sks(idx2d), b"".join(msgs), ctx=ctx))
+    for j, kind in sorted(plan.items()):
+        corrupt(sigs, idx2d, j, kind, B)
+    expect = np.ones(B, dtype=bool)
+    expect[list(plan)] = False
+    return idx2d, np.arange(B + 1, dtype=np.uint64) * n, msgs, sigs, expect
+
+
+# --------------------------------------------------------------- CPU baseline --
 _CPU = {}
 
 
@@ -156,7 +273,9 @@ def cpu_baseline(n: int, seconds: float, cores: int, reg_n: int = 1 << 14, per_c
         pass
     return {"value": round(rlc, 2), "unit": "FAV/s", "cores": cores, "kind": "port",
             "per_call_value": round(per_call, 2),
-            "sample": f"oracle/bls_oracle.c (C restatement, 6x64-bit Montgomery) on {cores} host processes ({cpu}): "
+            "sample": f"oracle/bls_oracle.c (C restatement, 6x64-bit Montgomery) on {cores} host processes ({cpu}; "
+                      f"the box's CPU share per GPU, OMP_NUM_THREADS -- its sched_getaffinity set is the whole "
+                      f"machine's, shared with the other GPUs' jobs): "
                       f"FastAggregateVerify(n={n}) over a {reg_n}-key pre-validated affine registry, {B} distinct "
                       f"aggregates cycled; RLC-batched per {per_core} calls: {res[1][0]} calls in {res[1][1]:.1f} s; "
                       f"per call (own final exponentiation, reference-equivalent): {res[0][0]} calls in "
@@ -166,7 +285,7 @@ def cpu_baseline(n: int, seconds: float, cores: int, reg_n: int = 1 << 14, per_c
 def percall_latency(reps: int = 15):
     """Median wall-clock latency of the drop-in per-call API (E/utils/bls.py:141-177 call pattern: one ctypes
     call per verification, host buffers): Verify and FastAggregateVerify(n = 512), beside the C port's per-call
-    time on one host core for the same inputs."""
+    time on one host core for the same inputs (checker only, outside every timed region)."""
     import statistics
 
     from bls_mi355x.backend import mi355x_bls as M
@@ -195,15 +314,72 @@ def percall_latency(reps: int = 15):
             "note": "median wall-clock per call incl. ctypes + H2D/D2H; CPU port = oracle/bls_oracle.c on 1 core"}
 
 
+# -------------------------------------------------------------------- parity --
+def parity_sample(batch, ctx, per_kind: int = 8, oracle_items: int = 16, seed: int = 0xA11):
+    """Untimed parity evidence for the bench line (rank 0): an adversarial C2 slice (1,024 x 512, per_kind bad
+    items of every SURVEY.md §8(d) kind) through the host-buffer batch API, its verdicts against the
+    construction and, on `oracle_items` sampled items, against the C oracle (oracle/bls_oracle.c, the checker);
+    hash_to_G2 of tests/golden/hash_to_g2.json against the committed points; the deposit-cli known answer
+    (E/test/capella/block_processing/test_process_bls_to_execution_change.py:257-288) through the per-call API."""
+    from bls_mi355x.backend import mi355x_bls as M
+    from oracle import bls_oracle_c as OC
+
+    B, n = 1024, 512
+    plan = adversarial_plan(B, per_kind, seed)
+    idx2d, offs, msgs, sigs, expect = adversarial_inputs(batch, ctx, B, n, plan, seed)
+    out = batch.fast_aggregate_verify_batch(idx2d.reshape(-1), offs, b"".join(msgs), bytes(sigs), ctx=ctx)
+    checks, rounds = batch.fallback_stats(ctx=ctx)
+    mism = int((out != expect).sum())
+    # the C oracle on the same compressed keys: one bad item of each kind + good ones
+    rng = np.random.default_rng(seed + 1)
+    bad_pick = [next(j for j in sorted(plan) if plan[j] == k) for k in BAD_KINDS]
+    good = [j for j in range(B) if expect[j]]
+    pick = bad_pick + [int(x) for x in rng.choice(good, size=oracle_items - len(bad_pick), replace=False)]
+    pk_of = {i: OC.SkToPk(i + 1) for i in sorted({int(x) for j in pick for x in idx2d[j] if x < REG_N})}
+    pk_of[IDX_INF], pk_of[IDX_0x40] = G1_INF, PK_0x40
+    o_mism = 0
+    for j in pick:
+        o = OC.FastAggregateVerify([pk_of[int(x)] for x in idx2d[j]], msgs[j], bytes(sigs[96 * j: 96 * j + 96]))
+        o_mism += int(bool(o) != bool(out[j]))
+    # hash_to_G2 golden points
+    with open(os.path.join(ROOT, "tests", "golden", "hash_to_g2.json")) as fh:
+        h2c = json.load(fh)
+    hb = lambda s: bytes.fromhex(s[2:] if s.startswith("0x") else s)  # noqa: E731
+    h_mism = sum(M.hash_to_G2(hb(c["msg"]), c["dst"].encode()) != hb(c["output"]) for c in h2c)
+    with open(os.path.join(ROOT, "tests", "golden", "known_answers.json")) as fh:
+        ka = json.load(fh)
+    k_mism = sum(M.Verify(hb(c["pubkey"]), hb(c["signing_root"]), hb(c["signature"])) != c["output"]
+                 for c in ka.values())
+    return {"items": B, "mismatches": mism + o_mism + h_mism + k_mism,
+            "batch": {"items": B, "bad": len(plan), "bad_kinds": list(BAD_KINDS), "per_kind": per_kind,
+                      "mismatches_vs_construction": mism, "fe_checks": checks, "bisection_rounds": rounds},
+            "oracle": {"items": len(pick), "mismatches": o_mism, "checker": "oracle/bls_oracle.c FastAggregateVerify"},
+            "hash_to_g2": {"points": len(h2c), "mismatches": int(h_mism), "source": "tests/golden/hash_to_g2.json"},
+            "known_answers": {"cases": len(ka), "mismatches": int(k_mism)}}
+
+
+# ---------------------------------------------------------------------- main --
+def _lib_sha() -> str | None:
+    try:
+        with open(LIB, "rb") as fh:
+            return hashlib.sha256(fh.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40, help="timed passes (4 in flight: fewer passes under-fill the pipeline)")
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2")
+    ap.add_argument("--steps", type=int, default=40, help="timed steps (4 in flight: fewer passes under-fill the pipeline)")
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=10000, help="FastAggregateVerify calls per GPU per step")
+    ap.add_argument("--batch", type=int, default=10000, help="C2: FastAggregateVerify calls per GPU per step")
     ap.add_argument("--committee", type=int, default=512)
-    ap.add_argument("--registry", type=int, default=1 << 20)
+    ap.add_argument("--registry", type=int, default=REG_N)
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--c4-total", type=int, default=C4_TOTAL)
+    ap.add_argument("--c5-bad", type=int, default=8, help="C5: bad items per batch (kinds cycled)")
+    ap.add_argument("--c3-steps", type=int, default=20, help="epochs timed for the c2 line's C3 figure (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight (no overlap of passes)")
@@ -211,6 +387,7 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) batch call")
     ap.add_argument("--roofline-passes", type=int, default=5, help="one-batch-at-a-time passes timed per kernel")
     ap.add_argument("--no-percall", action="store_true", help="skip the drop-in per-call latency figures")
+    ap.add_argument("--no-parity", action="store_true", help="skip the parity sample")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -227,11 +404,13 @@ def main():
 
     ctx = _native.context()
     dev_name, cus = ctx.device_info()
-    if dist is not None:
+    comm = dist is not None
+    if comm:
         from bls_mi355x import dist as bdist
         from torch.distributed import distributed_c10d as c10d
 
         bdist.init_comm(ctx, rank, world, c10d._get_default_store())
+        _COMM_CTX.append(ctx)
 
     def barrier_sync():
         ctx.check(ctx.lib.bls_sync(ctx.h))
@@ -242,63 +421,138 @@ def main():
                 torch.cuda.synchronize()
             dist.barrier()
 
-    # ---- setup (untimed) ----------------------------------------------------
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(rb, steps, warmup, depth=None):
+        """warmup + `steps` timed passes of rb between barriers; max over ranks; every pass must pass."""
+        d = 1 if args.no_pipeline else (batch.FAV_DEPTH if depth is None else depth)
+        if warmup:
+            rb.run_pipelined([os.urandom(32) for _ in range(warmup)], depth=d, comm=comm)
+        barrier_sync()
+        t0 = time.perf_counter()
+        oks = rb.run_pipelined([os.urandom(32) for _ in range(steps)], depth=d, comm=comm)
+        barrier_sync()
+        return max_over_ranks(time.perf_counter() - t0), oks
+
+    # ---- setup (untimed): registry 2^20 (sk_i = i + 1) + two invalid appended keys (C5 kinds) ----
     t_setup = time.perf_counter()
     reg = batch.Registry(ctx)
     reg.generate(args.registry, first_sk=1)
-    idx, offs, msgs, sks = build_inputs(args.batch, args.committee, args.registry, args.seed, rank)
-    sigs = batch.sign_batch(sks, msgs, ctx=ctx)
-    rb = batch.ResidentFavBatch(idx, offs, msgs, sigs, ctx=ctx)
-    setup_s = time.perf_counter() - t_setup
+    if args.registry == REG_N:
+        assert reg.append(G1_INF + PK_0x40).tolist() == [0, 0]
+    n = args.committee
+    extra = {}
+    rb = None
 
-    def passes(k: int, depth: int | None = None) -> list:
-        """k passes over the batch; by default pass j+1.. are submitted before pass j is final-exponentiated
-        (up to FAV_DEPTH batches in flight, bls_fav_job_*), so every pass completes inside the call."""
-        if args.no_pipeline:
-            depth = 1
-        d = batch.FAV_DEPTH if depth is None else depth
-        return rb.run_pipelined([os.urandom(32) for _ in range(k)], depth=d, comm=dist is not None)
+    if args.config == "c2":
+        B = args.batch
+        idx, offs, msgs, sks = build_inputs(B, n, args.registry, args.seed, rank)
+        sigs = batch.sign_batch(sks, msgs, ctx=ctx)
+        rb = batch.ResidentFavBatch(idx, offs, msgs, sigs, ctx=ctx)
+        setup_s = time.perf_counter() - t_setup
+        dt, oks = timed(rb, args.steps, args.warmup)
+        assert all(oks), "a valid C2 batch failed the pairing check"
+        v = rb.verdicts()
+        assert v.all(), f"{(~v).sum()} valid aggregates rejected"
+        units, unit, scaling = B * world, "FAV/s", "weak"
+        workload = f"C2 sync-committee FastAggregateVerify: {B} aggregates x {n} pubkeys per GPU"
+        ops_step = item_ops(n) * B * world + BATCH_OPS * world
+    elif args.config == "c3":
+        idx, offs, msgs, sks, (lo, hi) = c3_shard(args.registry, args.seed, rank, world)
+        B = hi - lo
+        rb = batch.ResidentFavBatch(idx, offs, msgs, batch.sign_batch(sks, msgs, ctx=ctx), ctx=ctx)
+        setup_s = time.perf_counter() - t_setup
+        dt, oks = timed(rb, args.steps, args.warmup)
+        assert all(oks) and rb.verdicts().all()
+        units, unit, scaling = C3_SLOTS * C3_PER_SLOT, "FAV/s", "strong"
+        workload = (f"C3 mainnet epoch replay: {C3_SLOTS} slots x {C3_PER_SLOT} committees of {C3_N} over a "
+                    f"2^20 registry, epoch sharded over {world} GPU(s), one RLC verdict per epoch")
+        ops_step = item_ops(C3_N) * units + BATCH_OPS * world
+        extra["ms_per_epoch"] = round(dt / args.steps * 1e3, 3)
+    elif args.config == "c4":
+        idx, offs, msgs, sks, chunks, (lo, hi) = c4_shard(args.c4_total, args.seed, rank, world)
+        B = hi - lo
+        rb = batch.ResidentFavBatch(idx, offs, msgs, batch.sign_batch(sks, msgs, ctx=ctx), ctx=ctx, chunks=chunks)
+        setup_s = time.perf_counter() - t_setup
+        dt, oks = timed(rb, args.steps, args.warmup)
+        assert all(oks) and rb.verdicts().all()
+        units, unit, scaling = args.c4_total, "Verify/s", "strong"
+        workload = (f"C4 gossip firehose: {args.c4_total} single-signature Verify (pk_i = registry[i], distinct "
+                    f"messages), contiguous shards of {B} per GPU in {chunks} job(s)")
+        ops_step = item_ops(1) * units + BATCH_OPS * chunks * world
+    else:  # c5
+        B = 1024
+        plan = {int(j): BAD_KINDS[t % len(BAD_KINDS)] for t, j in
+                enumerate(np.random.default_rng(args.seed + rank).choice(B, size=args.c5_bad, replace=False))}
+        idx2d, offs, msgs, sigs, expect = adversarial_inputs(batch, ctx, B, n, plan, args.seed + 17 * rank,
+                                                             args.registry)
+        rb = batch.ResidentFavBatch(idx2d.reshape(-1), offs, b"".join(msgs), bytes(sigs), ctx=ctx)
+        setup_s = time.perf_counter() - t_setup
+        dt, oks = timed(rb, args.steps, args.warmup)
+        assert (rb.verdicts() == expect).all(), "adversarial verdicts differ from the construction"
+        checks, rounds = batch.fallback_stats(ctx=ctx)
+        units, unit, scaling = B * world, "FAV/s", "weak"
+        workload = (f"C5 adversarial FAV batches: {B} x {n} per GPU with {args.c5_bad} bad items "
+                    f"({', '.join(sorted(set(plan.values())))}), bisection fallback every step")
+        ops_step = item_ops(n) * units + BATCH_OPS * world
+        extra["fallback_last_step"] = {"fe_checks": checks, "bisection_rounds": rounds}
+        if rank == 0:  # AggregateVerify with N distinct messages (drop-in per call, replicas per rank)
+            from bls_mi355x.backend import mi355x_bls as M
+            av = {}
+            for N in (128, 1024, 8192):
+                ks = [(7919 * (i + 1)) for i in range(N)]
+                pks = batch.sk_to_pk_batch(b"".join(k.to_bytes(32, "big") for k in ks), ctx=ctx)
+                pkl = [pks[48 * i: 48 * i + 48] for i in range(N)]
+                ms = [_msg(b"av", N, i) for i in range(N)]
+                s = batch.sign_batch(b"".join(k.to_bytes(32, "big") for k in ks), b"".join(ms), ctx=ctx)
+                agg = M.Aggregate([s[96 * i: 96 * i + 96] for i in range(N)])
+                assert M.AggregateVerify(pkl, ms, agg)
+                t = time.perf_counter()
+                ok = M.AggregateVerify(pkl, ms, agg)
+                av[str(N)] = {"pairs_s": round(N / (time.perf_counter() - t), 1), "ok": bool(ok)}
+            extra["aggregate_verify"] = av
 
-    if args.warmup:
-        assert all(passes(args.warmup)), "warmup batch failed the pairing check"
-    v = rb.verdicts()
-    assert v.all(), f"{(~v).sum()} valid aggregates rejected"
+    ms_step = dt / args.steps * 1e3
+    value = units * args.steps / dt
 
-    barrier_sync()
-    t0 = time.perf_counter()
-    oks = passes(args.steps)
-    barrier_sync()
-    dt = time.perf_counter() - t0
-    assert all(oks)
-    if dist is not None:
-        import torch
+    # ---- C3 epoch-replay figure beside the C2 headline (every rank: the epoch is sharded) ----
+    if args.config == "c2" and args.c3_steps > 0 and args.registry == REG_N:
+        idx3, offs3, msgs3, sks3, (lo3, hi3) = c3_shard(args.registry, args.seed, rank, world)
+        rb3 = batch.ResidentFavBatch(idx3, offs3, msgs3, batch.sign_batch(sks3, msgs3, ctx=ctx), ctx=ctx)
+        dt3, oks3 = timed(rb3, args.c3_steps, 2)
+        assert all(oks3) and rb3.verdicts().all()
+        e = C3_SLOTS * C3_PER_SLOT
+        extra["c3"] = {"fav_s": round(e * args.c3_steps / dt3, 1), "ms_per_epoch": round(dt3 / args.c3_steps * 1e3, 3),
+                       "epochs": args.c3_steps, "shard": [lo3, hi3],
+                       "workload": f"{C3_SLOTS} slots x {C3_PER_SLOT} committees of {C3_N} (2^20 registry), "
+                                   f"one RLC verdict per epoch, epochs pipelined like C2"}
+        rb3.free()
 
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
     # per-kernel execution times: one batch at a time, hipEvents around each launch (after the timed region)
     kern = {}
-    if not args.no_profile and args.roofline_passes > 0:
+    if not args.no_profile and args.roofline_passes > 0 and rb is not None and rb.chunks == 1:
         prof = batch.Profiler(ctx)
         prof.start()
-        assert all(passes(args.roofline_passes, depth=1))
+        rb.run_pipelined([os.urandom(32) for _ in range(args.roofline_passes)], depth=1, comm=comm)
         kern = prof.read()
         prof.stop()
-    B, n = args.batch, args.committee
-    ms_step = dt / args.steps * 1e3
-    value = B * world * args.steps / dt
 
     # ---- roofline: dominant kernel, algorithmic int ops per launch -----------
-    fme = model_fme(n)
+    fme = model_fme(n if args.config != "c4" else 1)
     roof = None
     kernels_ms = {k: round(v[0] / max(v[1], 1), 4) for k, v in kern.items() if v[1]}
+    per_launch = rb.cb if rb is not None else 0  # items per FAV job (one launch of each kernel)
     if kern:
-        # candidates: the profile entries that time exactly one kernel (k_miller_lane, k_fav_gather<16>), so the
-        # rocprofv3 summary's average for that kernel can be set beside this hipEvent figure
         dom = max((k for k in SINGLE_KERNEL if k in kern and kern[k][1]), key=lambda k: kern[k][0])
         avg_s = kern[dom][0] / kern[dom][1] * 1e-3
-        units = B
-        ops = round(fme[dom] * FME_OPS * units) + (19 * SHA_OPS * B if dom == "fav_hash" else 0)
+        ops = round(fme[dom] * FME_OPS * per_launch)
         ach = ops / avg_s / 1e12
         traffic, tsrc = None, None
         try:  # HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE pass (a PMC run cannot be live)
@@ -309,61 +563,66 @@ def main():
             pass
         roof = {"bound": "valu-int", "kernel": dom, "symbol": KERNEL_SYMBOL.get(dom), "achieved": round(ach, 4),
                 "peak": round(PEAK_INT_OPS / 1e12, 2), "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5),
+                "frac_source": f"this run: algorithmic ops / hipEvent launch time ({args.roofline_passes} "
+                               f"one-batch-at-a-time passes after the timed region)",
                 "traffic": traffic, "traffic_source": tsrc, "ops_per_launch": ops,
-                "avg_launch_ms": round(avg_s * 1e3, 4),
-                "avg_source": f"hipEvents around each launch, {args.roofline_passes} one-batch-at-a-time passes"}
-        try:  # the committed rocprofv3 --kernel-trace --stats average of the same kernel (same build)
+                "avg_launch_ms": round(avg_s * 1e3, 4)}
+        try:  # the committed rocprofv3 --kernel-trace --stats average of the same kernel -- only for the same build
             with open(ROCPROF_AVG) as fh:
                 rj = json.load(fh)
             r_ms = rj["avg_ms"].get(KERNEL_SYMBOL.get(dom))
-            if r_ms:
+            if r_ms and rj.get("lib_sha256_16") and rj["lib_sha256_16"] == _lib_sha():
                 roof["rocprof_avg_ms"] = r_ms
-                roof["rocprof_source"] = rj["source"]
+                roof["rocprof_source"] = rj["source"] + " (committed profile of this exact libblsmi355x.so)"
                 roof["frac_rocprof"] = round(ops / (r_ms * 1e-3) / PEAK_INT_OPS, 5)
         except (OSError, ValueError, KeyError):
             pass
-    if roof is not None:
         roof["frac_of_measured_mad_rate"] = round(roof["achieved"] * 1e12 / MEASURED_MAD_OPS, 5)
         if dom in LANE_KERNELS:  # k lanes per item, one wave per SIMD: the launch holds ceil(k B / 64) SIMDs
-            occ = min(1.0, ((LANE_KERNELS[dom] * B + 63) // 64) / (cus * 4))
+            occ = min(1.0, ((LANE_KERNELS[dom] * per_launch + 63) // 64) / (cus * 4))
             roof["occupied_simd_frac"] = round(occ, 4)
             roof["frac_of_occupied_simds"] = round(roof["frac"] / occ, 4)
     # secondary figure: algorithmic HBM bytes of the registry gather per launch / its duration
     gather_gbs = None
     if "fav_gather" in kern and kern["fav_gather"][1]:
         g_s = kern["fav_gather"][0] / kern["fav_gather"][1] * 1e-3
-        gather_gbs = round(B * n * GATHER_BYTES_PER_KEY / g_s / 1e9, 1)
+        keys = per_launch * (n if args.config != "c4" else 1)
+        gather_gbs = round(keys * GATHER_BYTES_PER_KEY / g_s / 1e9, 1)
     # PCIe-inclusive rate: the host-buffer C-ABI call (bls_fav_batch_indexed: inputs copied H2D, verdicts D2H),
     # one batch at a time, no pipelining.  Reported beside `value`, never as it.
     e2e = None
-    if rank == 0 and not args.no_e2e:
+    if rank == 0 and not args.no_e2e and args.config == "c2":
         batch.fast_aggregate_verify_batch(idx, offs, msgs, sigs, ctx=ctx)
         t1 = time.perf_counter()
         v2 = batch.fast_aggregate_verify_batch(idx, offs, msgs, sigs, ctx=ctx)
-        e2e = round(B / (time.perf_counter() - t1), 1)
+        e2e = round(args.batch / (time.perf_counter() - t1), 1)
         assert v2.all()
+    barrier_sync()
     percall = None
     if rank == 0 and world == 1 and not args.no_percall:
         percall = percall_latency()
-    total_fme = 11 * n + 14789
-    pipeline_ops = (total_fme * FME_OPS + 19 * SHA_OPS) * B * world * args.steps + 9268 * FME_OPS * args.steps
-    pipeline_frac = pipeline_ops / dt / (PEAK_INT_OPS * world)
+    parity = None
+    if rank == 0 and not args.no_parity and args.registry == REG_N:
+        parity = parity_sample(batch, ctx)
+    pipeline_frac = ops_step * args.steps / dt / (PEAK_INT_OPS * world)
 
     out = {
-        "metric": METRIC, "value": round(value, 2), "unit": "FAV/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u32-limb Fp (381-bit Montgomery)",
+        "metric": METRIC, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": scaling,
+        "vs_baseline": None, "dtype": "u32 (381-bit Montgomery Fp, radix-2^29 digits)",
         "data": "synthetic: registry sk_i=i+1 (2^20 keys, HBM), SHA256 messages, signatures made on device",
-        "config": {"workload": f"C2 sync-committee FastAggregateVerify: {B} aggregates x {n} pubkeys per GPU",
-                   "global_batch": B * world, "committee": n, "registry": args.registry,
-                   "parallelism": f"dp{world} (aggregates sharded, RCCL all-gather of 576-B Fp12 partials)"},
+        "config": {"workload": workload, "config": args.config,
+                   "global_batch": units, "committee": n if args.config != "c4" else 1, "registry": args.registry,
+                   "parallelism": f"dp{world} (sharded, RCCL all-gather of 576-B Fp12 partials)"},
         "roofline": roof,
         "int_valu_frac_pipeline": round(pipeline_frac, 5),
+        "parity": parity,
+        **extra,
         "kernels_avg_ms": kernels_ms,
         "gather_hbm_gbs": gather_gbs,
         "host_buffers_fav_s": e2e,
         "percall": percall,
-        "device": dev_name, "cus": cus, "setup_s": round(setup_s, 2),
+        "device": dev_name, "cus": cus, "setup_s": round(setup_s, 2), "lib_sha256_16": _lib_sha(),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         cores = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or 1 << 30, len(os.sched_getaffinity(0)))
@@ -372,11 +631,22 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    rb.free()
+    barrier_sync()  # rank 0's untimed legs (percall, parity, CPU) are done before any rank tears down
+    if rb is not None:
+        rb.free()
     if dist is not None:
+        _COMM_CTX.clear()
         bdist.destroy_comm(ctx)
         dist.destroy_process_group()
 
 
+_COMM_CTX: list = []  # the context whose RCCL communicator is live (aborted if this rank fails)
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:
+        if _COMM_CTX:  # peers blocked in an all-gather with this rank fail instead of hanging
+            from bls_mi355x import dist as _bd
+            _bd.abort_comm(_COMM_CTX[0])
+        raise

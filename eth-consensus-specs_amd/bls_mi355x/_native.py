@@ -104,6 +104,7 @@ _SIGS = {
     "bls_comm_init": (_ip, [_vp, _u8p, _ip, _ip]),
     "bls_comm_destroy": (_ip, [_vp]),
     "bls_fav_job_check_comm": (_ip, [_vp, _ip]),
+    "bls_comm_abort": (_ip, [_vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -23,6 +23,7 @@ from . import _native
 FAV_JOBS = max(1, min(8, int(os.environ.get("BLS_FAV_JOBS_INIT", "5"))))
 # batches kept in flight by run_pipelined (<= FAV_JOBS)
 FAV_DEPTH = max(1, min(FAV_JOBS, int(os.environ.get("BLS_FAV_DEPTH", str(FAV_JOBS)))))
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # the BLS12-381 group order r
 
 
 def _ptr(a: np.ndarray):
@@ -249,6 +250,9 @@ def g1_multi_exp(points48, scalars, ctx=None, subgroup_check: bool = False) -> b
         raise ValueError("one scalar per point")
     if any(len(p) != 48 for p in pts) or any(not 0 <= k < 1 << 256 for k in ks):
         raise ValueError("need 48-byte points and 256-bit scalars")
+    # reduced mod r as curve.Scalar / curve._k32 do (arkworks' Scalar): for a point decoded without the subgroup
+    # check, [k]P and [k mod r]P differ, and both entry points must give the same result
+    ks = [k % R_ORDER for k in ks]
     out = ctypes.create_string_buffer(48)
     rc = c.check(c.lib.bls_multi_exp(c.h, 1, b"".join(pts), b"".join(k.to_bytes(32, "big") for k in ks), len(pts),
                                      1 if subgroup_check else 0, out))
@@ -317,18 +321,34 @@ class ResidentFavBatch:
     final-exponentiated by ``check_partials``; ``finish()`` writes verdicts.
     """
 
-    def __init__(self, indices, offsets, msgs32, sigs96, ctx=None):
+    def __init__(self, indices, offsets, msgs32, sigs96, ctx=None, chunks: int = 1):
+        """chunks > 1 splits the batch into that many equal sub-batches (uniform committee size only), each
+        submitted as its own FAV job: a pass over the batch is `chunks` jobs (large shards, e.g. the C4 firehose,
+        stay within one job's scratch)."""
         self.ctx = ctx or _native.context()
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.B = int(offs.size - 1)
+        self.chunks = max(1, int(chunks))
+        if self.chunks > 1:
+            n = int(offs[1] - offs[0]) if self.B else 0
+            if self.B % self.chunks or not np.array_equal(offs, np.arange(self.B + 1, dtype=np.uint64) * n):
+                raise ValueError("chunks > 1 needs B divisible by chunks and one committee size")
+            self.cb, self.n = self.B // self.chunks, n
+            offs = offs[: self.cb + 1]  # every chunk has the same relative offsets
+        else:
+            self.cb, self.n = self.B, None
         self.idx = DeviceBuffer(self.ctx, np.ascontiguousarray(indices, dtype=np.uint32))
-        self.offs = DeviceBuffer(self.ctx, np.ascontiguousarray(offsets, dtype=np.uint64))
-        self.B = int(np.asarray(offsets).size - 1)
+        self.offs = DeviceBuffer(self.ctx, offs)
         self.msgs = DeviceBuffer(self.ctx, _u8(msgs32))
         self.sigs = DeviceBuffer(self.ctx, _u8(sigs96))
         self.outs = [DeviceBuffer(self.ctx, nbytes=self.B) for _ in range(FAV_JOBS)]
         self.out = self.outs[0]
         self.last_job = 0
+        self._chunk_job = [0] * self.chunks  # job whose buffer holds each chunk's latest verdicts
 
     def partial(self, seed32: bytes | None = None) -> bytes:
+        if self.chunks > 1:
+            raise ValueError("a chunked batch runs through the job API (run_pipelined)")
         seed = seed32 if seed32 is not None else os.urandom(32)
         buf = ctypes.create_string_buffer(576)
         c = self.ctx
@@ -347,10 +367,15 @@ class ResidentFavBatch:
         self.last_job = 0
 
     # ---- pipelined passes (bls_fav_job_*): up to FAV_JOBS batches in flight --
-    def submit(self, job: int, seed32: bytes) -> None:
+    def _chunk_ptrs(self, c: int):
+        lo = c * self.cb
+        nidx = lo * self.n if self.chunks > 1 else 0
+        return self.idx.ptr + 4 * nidx, self.msgs.ptr + 32 * lo, self.sigs.ptr + 96 * lo, lo
+
+    def submit(self, job: int, seed32: bytes, chunk: int = 0) -> None:
         c = self.ctx
-        c.check(c.lib.bls_fav_job_submit_dev(c.h, job, self.idx.ptr, self.offs.ptr, self.B, self.msgs.ptr,
-                                             self.sigs.ptr, seed32))
+        idx, msgs, sigs, _ = self._chunk_ptrs(chunk)
+        c.check(c.lib.bls_fav_job_submit_dev(c.h, job, idx, self.offs.ptr, self.cb, msgs, sigs, seed32))
 
     def job_partial(self, job: int) -> bytes:
         buf = ctypes.create_string_buffer(576)
@@ -362,10 +387,12 @@ class ResidentFavBatch:
         c = self.ctx
         return c.check(c.lib.bls_fav_job_check(c.h, job, partials, len(partials) // 576)) == 1
 
-    def job_finish(self, job: int, batch_ok: bool) -> None:
+    def job_finish(self, job: int, batch_ok: bool, chunk: int = 0) -> None:
         c = self.ctx
-        c.check(c.lib.bls_fav_job_finish_dev(c.h, job, 1 if batch_ok else 0, self.outs[job].ptr))
+        lo = self._chunk_ptrs(chunk)[3]
+        c.check(c.lib.bls_fav_job_finish_dev(c.h, job, 1 if batch_ok else 0, self.outs[job].ptr + lo))
         self.last_job = job
+        self._chunk_job[chunk] = job
 
     def job_check_comm(self, job: int) -> bool:
         """RCCL all-gather of the job's device-resident partial + the product's final exponentiation
@@ -374,33 +401,39 @@ class ResidentFavBatch:
         return c.check(c.lib.bls_fav_job_check_comm(c.h, job)) == 1
 
     def run_pipelined(self, seeds, exchange=None, depth: int = FAV_DEPTH, comm: bool = False) -> list:
-        """One pass over the batch per seed with up to `depth` passes in flight:
-        pass k+1.. are submitted before pass k is final-exponentiated (their
-        front kernels overlap pass k's tail).  Multi-GPU: comm=True exchanges
-        the partials inside the library over RCCL (bls_fav_job_check_comm);
-        otherwise exchange(partial) -> concatenated partials of all ranks (a
-        host-side all-gather, e.g. gloo in the CPU tests).  Every pass is
-        complete (verdicts written) on return."""
+        """One pass over the batch per seed (a pass = `chunks` jobs) with up to `depth` jobs in flight:
+        job k+1.. are submitted before job k is final-exponentiated (their front kernels overlap job k's
+        tail).  Multi-GPU: comm=True exchanges each job's partial inside the library over RCCL
+        (bls_fav_job_check_comm); otherwise exchange(partial) -> concatenated partials of all ranks (a
+        host-side all-gather, e.g. gloo in the CPU tests).  Every pass is complete (verdicts written) on
+        return; returns one bool per pass (all of its chunks' batch checks passed)."""
         seeds = list(seeds)
         depth = max(1, min(depth, FAV_JOBS))
-        oks = []
-        for k in range(min(depth, len(seeds))):
-            self.submit(k % FAV_JOBS, seeds[k])
-        for k in range(len(seeds)):
-            job = k % FAV_JOBS
+        units = [(k, ch) for k in range(len(seeds)) for ch in range(self.chunks)]
+        oks = [True] * len(seeds)
+        for u in range(min(depth, len(units))):
+            k, ch = units[u]
+            self.submit(u % FAV_JOBS, seeds[k], ch)
+        for u, (k, ch) in enumerate(units):
+            job = u % FAV_JOBS
             if comm:
                 ok = self.job_check_comm(job)
             else:
                 part = self.job_partial(job)
                 ok = self.job_check(job, exchange(part) if exchange else part)
-            self.job_finish(job, ok)
-            oks.append(ok)
-            if k + depth < len(seeds):
-                self.submit((k + depth) % FAV_JOBS, seeds[k + depth])
+            self.job_finish(job, ok, ch)
+            oks[k] = oks[k] and ok
+            if u + depth < len(units):
+                k2, ch2 = units[u + depth]
+                self.submit((u + depth) % FAV_JOBS, seeds[k2], ch2)
         return oks
 
     def verdicts(self) -> np.ndarray:
-        return self.outs[self.last_job].to_host().astype(bool)
+        if self.chunks == 1:
+            return self.outs[self.last_job].to_host().astype(bool)
+        bufs = {j: self.outs[j].to_host() for j in set(self._chunk_job)}
+        return np.concatenate([bufs[j][c * self.cb:(c + 1) * self.cb] for c, j in enumerate(self._chunk_job)]
+                              ).astype(bool)
 
     def run(self) -> np.ndarray:
         ok = self.check_partials(self.partial())

@@ -40,6 +40,12 @@ def destroy_comm(ctx: _native.Context) -> None:
     ctx.check(ctx.lib.bls_comm_destroy(ctx.h))
 
 
+def abort_comm(ctx: _native.Context) -> None:
+    """ncclCommAbort: peers blocked in a collective with this rank fail instead of hanging (call on an error
+    path before leaving the exchange)."""
+    ctx.lib.bls_comm_abort(ctx.h)
+
+
 def shard_bounds(total: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous, balanced [lo, hi) block of `total` items owned by `rank`."""
     base, extra = divmod(total, world)

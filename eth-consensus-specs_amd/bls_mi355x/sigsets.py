@@ -37,8 +37,11 @@ valid (test_process_deposit.py:255-287).  Returning a recorded True there
 would apply the deposit and then reject the block.  So ``try_defer`` looks at
 the caller's bytecode: the call is deferred only if its value flows, through
 ``return`` statements only, into an ``assert`` (``POP_JUMP_IF_TRUE`` followed
-by ``LOAD_ASSERTION_ERROR``); any other use -- ``if``, ``not``, a comparison,
-an assignment -- runs the call at once and returns its real verdict.
+by ``LOAD_ASSERTION_ERROR``), and every caller on the way calls exactly the
+function below it (no C-level caller such as ``map`` or ``any`` in between);
+any other use -- ``if``, ``not``, a comparison, an assignment -- runs the call
+at once and returns its real verdict.  The bytecode reading is for Python
+3.10 (this image's interpreter); on other versions every call runs at once.
 """
 from __future__ import annotations
 
@@ -55,30 +58,116 @@ FAV, VERIFY, AV = "fav", "verify", "av"
 
 _CODE_INDEX: dict = {}  # code object -> (instructions, {offset: position})
 
+# Python 3.10 stack effects (pops, pushes) of the opcodes that build call expressions; a span with any other
+# opcode is not simulated (the call then runs at once -- never a wrong verdict, only no batching)
+_LOADS = {"LOAD_GLOBAL", "LOAD_NAME", "LOAD_FAST", "LOAD_DEREF", "LOAD_CONST", "LOAD_CLOSURE", "LOAD_CLASSDEREF"}
+_FIXED = {"LOAD_ATTR": (1, 1), "LOAD_METHOD": (1, 2), "BINARY_SUBSCR": (2, 1), "COMPARE_OP": (2, 1),
+          "IS_OP": (2, 1), "CONTAINS_OP": (2, 1), "UNARY_NOT": (1, 1), "UNARY_NEGATIVE": (1, 1),
+          "UNARY_INVERT": (1, 1), "UNARY_POSITIVE": (1, 1), "LIST_TO_TUPLE": (1, 1), "GET_ITER": (1, 1),
+          "DUP_TOP": (1, 2), "NOP": (0, 0), "DICT_MERGE": (1, 0), "DICT_UPDATE": (1, 0), "LIST_EXTEND": (1, 0),
+          "SET_UPDATE": (1, 0), "LIST_APPEND": (1, 0), "SET_ADD": (1, 0), "MAP_ADD": (2, 0)}
 
-def _next_ops(code, lasti: int, k: int = 2) -> list[str]:
-    """Opnames of the k instructions after the one at byte offset `lasti` ([] if unknown)."""
+
+def _index(code):
     ent = _CODE_INDEX.get(code)
     if ent is None:
         ins = list(dis.get_instructions(code))
         ent = (ins, {x.offset: i for i, x in enumerate(ins)})
         _CODE_INDEX[code] = ent
-    ins, pos = ent
+    return ent
+
+
+def _next_ops(code, lasti: int, k: int = 2) -> list[str]:
+    """Opnames of the k instructions after the one at byte offset `lasti` ([] if unknown); TO_BOOL (3.13+,
+    before a conditional jump) is skipped."""
+    ins, pos = _index(code)
     i = pos.get(lasti)
     if i is None:
         return []
-    return [x.opname for x in ins[i + 1: i + 1 + k]]
+    return [x.opname for x in ins[i + 1:] if x.opname != "TO_BOOL"][:k]
 
 
-def result_is_asserted(frame) -> bool:
-    """True iff the value returned to `frame` by the call it is executing reaches an ``assert`` through
-    ``return`` statements only (walking up the callers)."""
+def _pops_pushes(x):
+    op, a = x.opname, x.arg
+    if op in _LOADS:
+        return 0, 1
+    if op in _FIXED:
+        return _FIXED[op]
+    if op.startswith("BINARY_") or op.startswith("INPLACE_"):
+        return 2, 1
+    if op in ("BUILD_TUPLE", "BUILD_LIST", "BUILD_SET", "BUILD_STRING", "BUILD_SLICE"):
+        return a, 1
+    if op == "BUILD_MAP":
+        return 2 * a, 1
+    if op == "BUILD_CONST_KEY_MAP":
+        return a + 1, 1
+    if op == "CALL_FUNCTION":
+        return a + 1, 1
+    if op in ("CALL_FUNCTION_KW", "CALL_METHOD"):
+        return a + 2, 1
+    if op == "CALL_FUNCTION_EX":
+        return 2 + (a & 1), 1
+    if op == "FORMAT_VALUE":
+        return 1 + (1 if (a & 4) else 0), 1
+    return None
+
+
+def callee_name(code, lasti: int) -> str | None:
+    """Name of the callable invoked by the call instruction at byte offset `lasti` (Python 3.10 bytecode), or
+    None when it cannot be determined: the straight-line span back to the nearest jump target is simulated
+    with a symbolic stack whose entries remember the name they were loaded under (``bls.Verify`` ->
+    "Verify", ``is_valid_indexed_attestation`` -> itself, ``any`` -> "any")."""
+    if sys.version_info[:2] != (3, 10):
+        return None
+    ins, pos = _index(code)
+    i = pos.get(lasti)
+    if i is None or not ins[i].opname.startswith("CALL_"):
+        return None
+    lo = i
+    while lo > 0 and not ins[lo].is_jump_target:
+        lo -= 1
+    stack: list = []  # producer name per entry; the entries below the span are unknown (None)
+    for x in ins[lo:i]:
+        if "JUMP" in x.opname or x.opname in ("RETURN_VALUE", "FOR_ITER", "SETUP_FINALLY", "SETUP_WITH"):
+            stack = []  # control flow inside the span: nothing below is known
+            continue
+        pp = _pops_pushes(x)
+        if pp is None:
+            return None
+        pops, pushes = pp
+        if x.opname == "DUP_TOP":
+            top = stack[-1] if stack else None
+            stack.append(top)
+            continue
+        for _ in range(pops):
+            if stack:
+                stack.pop()
+        name = x.argval if x.opname in _LOADS or x.opname in ("LOAD_ATTR", "LOAD_METHOD") else None
+        if x.opname == "LOAD_METHOD":
+            stack.extend([name, None])  # (method, self) / (NULL, callable)
+        else:
+            stack.extend([name if isinstance(name, str) else None] * pushes)
+    pops, _ = _pops_pushes(ins[i])
+    if len(stack) < pops:
+        return None
+    return stack[-pops]
+
+
+def result_is_asserted(frame, callee: str) -> bool:
+    """True iff the value that the call to `callee` (the function `frame` is executing a call into) returns
+    reaches an ``assert`` through ``return`` statements only, walking up the callers.  At every level the
+    caller's instruction must be a call of exactly that function: a C-level caller in between (``map``,
+    ``any``, ``sorted`` ...) leaves no Python frame, so ``assert any(map(bls.Verify, ...))`` shows a call of
+    ``any`` there and the verdict is computed at once."""
     depth = 0
     while frame is not None and depth < 32:
+        if callee_name(frame.f_code, frame.f_lasti) != callee:
+            return False
         ops = _next_ops(frame.f_code, frame.f_lasti)
         if not ops:
             return False
         if ops[0] == "RETURN_VALUE":
+            callee = frame.f_code.co_name
             frame = frame.f_back
             depth += 1
             continue
@@ -114,7 +203,10 @@ class SignatureSets:
         """Called by the shim's Verify / FastAggregateVerify / AggregateVerify (bls.py ``_defer``): record the
         call and return True when its result is only asserted; otherwise False (the shim verifies at once)."""
         shim_fn = sys._getframe(2)  # try_defer <- bls._defer <- bls.Verify / ...
-        if not result_is_asserted(shim_fn.f_back):
+        caller = shim_fn.f_back  # only_with_bls's wrapper (named like the shim function), calling it as `fn`
+        callee = "fn" if caller is not None and caller.f_code.co_name == shim_fn.f_code.co_name else \
+            shim_fn.f_code.co_name
+        if not result_is_asserted(caller, callee):
             self.eager += 1
             return False
         {VERIFY: self.add_verify, FAV: self.add_fast_aggregate_verify, AV: self.add_aggregate_verify}[kind](*args)

@@ -33,6 +33,9 @@ enum Slot {
   S_KZ_IN, S_KZ_P, S_KZ_Q, S_KZ_OK, S_KZ_OK2, S_KZ_F, S_KZ_FT, S_KZ_S, S_KZ_J, S_KZ_OUT,
   // curve objects (bls_g1_* / bls_g2_* / bls_multi_exp / bls_multi_pairing / bls_gt_mul)
   S_PT_IN, S_PT_A, S_PT_OK, S_PT_TMP, S_PT_OUT,
+  // per-call Verify / FastAggregateVerify pair points (not S_RP: a FAV batch's r_i apk_i live there between its
+  // partial and finish calls, and fav_bisect reads them back)
+  S_PC_P,
   NSLOT
 };
 
@@ -424,7 +427,7 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_OFFS, 2, d_offs);
   SCR(S_G1A, n, keys);
   SCR(S_OK, n + 2, ok);  // key verdicts | sig verdict | live
-  SCR(S_RP, 2, P);
+  SCR(S_PC_P, 2, P);
   SCR(S_G2A, 2, Q);
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
@@ -1690,13 +1693,23 @@ int bls_comm_destroy(bls_ctx* ctx) {
 // 1 / 0.  The host never sees the partials.  Every rank must call this for the
 // same jobs in the same order (one outstanding collective at a time: the call
 // waits for the verdict).
-int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
-  JOB_ENTER(ctx, job);
-  Job& J = *ctx->j;
-  if (!ctx->comm) {
-    ctx->err = "bls_comm_init was not called";
-    return BLS_E_ARG;
+static int comm_abort_locked(bls_ctx* ctx) {
+  if (ctx->comm) {
+    (void)ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
   }
+  ctx->comm_rank = 0;
+  ctx->comm_world = 1;
+  return 0;
+}
+
+int bls_comm_abort(bls_ctx* ctx) {
+  API_ENTER(ctx);
+  return comm_abort_locked(ctx);
+}
+
+static int job_check_comm(bls_ctx* ctx) {
+  Job& J = *ctx->j;
   if (!J.partial_pending || !J.buf[S_BYTES].p) {
     ctx->err = "no submitted FAV batch on this job";
     return BLS_E_ARG;
@@ -1712,6 +1725,19 @@ int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
   J.partial_pending = false;  // consumed on the device (the pinned host copy is not waited for)
   PROF(9, launch_fp12_from_bytes(J.stream, d_all, W, f));
   return run_final_check(ctx, f, W);
+}
+
+int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
+  JOB_ENTER(ctx, job);
+  if (!ctx->comm) {
+    ctx->err = "bls_comm_init was not called";
+    return BLS_E_ARG;
+  }
+  const int r = job_check_comm(ctx);
+  // an error after the communicator exists leaves the peers waiting in this or a later all-gather: abort it so
+  // their collectives fail instead of hanging (the host sees this rank's negative code)
+  if (r < 0) comm_abort_locked(ctx);
+  return r;
 }
 
 }  // extern "C"

@@ -253,6 +253,12 @@ int bls_comm_unique_id(uint8_t* out128);
 int bls_comm_init(bls_ctx* ctx, const uint8_t* uid128, int rank, int world);
 int bls_comm_destroy(bls_ctx* ctx);
 int bls_fav_job_check_comm(bls_ctx* ctx, int job);
+/* Abort the communicator (ncclCommAbort): peers blocked in a collective with
+ * this rank fail instead of hanging.  The library calls it itself when
+ * bls_fav_job_check_comm fails after the communicator exists; a host that
+ * leaves the exchange on its own error (bench.py, dist.py) calls it before
+ * exiting.  No-op without a communicator. */
+int bls_comm_abort(bls_ctx* ctx);
 
 /* ---- tracing: hipEvent time per kernel of the FAV path ------------------ */
 int bls_profile_enable(bls_ctx* ctx, int on);  /* also resets the totals */

@@ -295,3 +295,23 @@ def test_resident_batch_pipelined(batch):
     assert good.run_pipelined([b"\x07" * 32, b"\x08" * 32], exchange=lambda p: p + p) == [True, True]
     good.free()
     bad.free()
+
+
+def test_percall_between_job_partial_and_finish(B, batch):
+    """A per-call Verify / FastAggregateVerify on job 0 while a job-0 FAV batch sits between its partial and
+    finish steps must not touch that batch's state: the bisection reads r_i apk_i back (the
+    per-call pair points used to share the batch's slot, so items 0 and 1 came back invalid)."""
+    pks, idx, offs, msgs, sigs = _synthetic(128, [8] * 10, seed=13)
+    batch.Registry().load(pks)
+    sigs[96 * 3: 96 * 4] = sigs[96 * 4: 96 * 5]  # item 3 invalid: the finish step bisects
+    rb = batch.ResidentFavBatch(idx, offs, b"".join(msgs), bytes(sigs))
+    rb.submit(0, b"\x09" * 32)
+    ok = rb.job_check(0, rb.job_partial(0))
+    assert ok is False
+    m = b"\x12" * 32
+    assert B.Verify(O.SkToPk(7), m, O.Sign(7, m)) is True
+    assert B.FastAggregateVerify([O.SkToPk(5), O.SkToPk(6)], m, O.Sign(11, m)) is True
+    rb.job_finish(0, ok)
+    v = rb.verdicts()
+    assert list(v) == [True] * 3 + [False] + [True] * 6
+    rb.free()

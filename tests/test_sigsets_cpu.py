@@ -149,7 +149,7 @@ from bls_mi355x.sigsets import result_is_asserted
 
 
 def probe():
-    return result_is_asserted(sys._getframe(1))
+    return result_is_asserted(sys._getframe(1), "probe")
 
 
 def asserted():
@@ -181,6 +181,22 @@ def branched():
 def stored():
     x = probe()
     return x
+
+
+def via_map():
+    assert not any(map(lambda _: probe(), [0]))
+
+
+def via_sorted():
+    assert not sorted([probe()])[0]
+
+
+def nested_arg(f):
+    assert f(probe())
+
+
+def in_conditional(c):
+    assert (probe() if c else False) or True
 """
 
 
@@ -192,6 +208,28 @@ def test_result_is_asserted_bytecode_patterns():
     ns["through_return"]()
     ns["negated"]()  # `assert not f()`: f must see False (deferring would return True and fail the assert)
     assert ns["branched"]() is False and ns["stored"]() is False and ns["returned"]() is False
+    ns["via_map"]()  # C-level callers (map / any) in between: the call runs at once (False here)
+    ns["via_sorted"]()
+    ns["nested_arg"](lambda v: v is False)  # probe() is an argument of f, not the asserted call
+    ns["in_conditional"](True)
+
+
+def test_callee_name_reads_the_call():
+    import dis
+    import sys as _sys
+
+    from bls_mi355x.sigsets import callee_name
+
+    if _sys.version_info[:2] != (3, 10):
+        pytest.skip("bytecode simulation is for Python 3.10")
+
+    ns = {}  # compiled from source: pytest rewrites this module's asserts
+    exec(compile("def f(bls, x, g):\n    assert bls.Verify(x, g(x), 3)\n    return any(map(bls.Verify, x))\n",
+                 "<f>", "exec"), ns)
+    f = ns["f"]
+    calls = [i for i in dis.get_instructions(f) if i.opname.startswith("CALL_")]
+    names = [callee_name(f.__code__, c.offset) for c in calls]
+    assert names == ["g", "Verify", "map", "any"]
 
 
 def test_wrong_lengths_are_false_not_errors(fakes):
