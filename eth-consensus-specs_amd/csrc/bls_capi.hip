@@ -21,12 +21,12 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_U, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
+  S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
   S_AV_IO, S_AV_RSC, S_AV_PITEM, S_AV_SIG, S_AV_SOK, S_AV_H, S_AV_ST, S_AV_P, S_AV_Q, S_AV_F, S_AV_FT, S_AV_SEL,
-  S_AV_FI, S_AV_RES, S_AV_U, S_AV_HCF, S_AV_FLAG, S_AV_ML,
+  S_AV_FI, S_AV_RES, S_AV_HCF, S_AV_FLAG, S_AV_ML,
   // signing roots / merkleization
   S_SZ_A, S_SZ_B, S_SZ_C, S_SZ_Z,
   // KZG pieces
@@ -417,7 +417,6 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   G2A* Q;
   int *ok, *d_r;
   G1J *tmp, *apk;
-  Fp* U;
   Fd* hf;
   int* flag;
   Fp12* f;
@@ -431,7 +430,6 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_G2A, 2, Q);
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
-  SCR(S_AV_U, 8, U);
   SCR(S_AV_HCF, h2c_scratch_fd(1), hf);
   SCR(S_AV_FLAG, 1, flag);
   SCR(S_F, 1, f);
@@ -447,7 +445,7 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
-  LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, U, hf, Q, flag));
+  LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, hf, Q, flag));
   CK(h2c_fallback(ctx, st2, 1, d_msg, d_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
@@ -466,26 +464,10 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   return (live && fe) ? 1 : 0;
 }
 
-static bool percall_lane() {  // A/B knob: the previous one-lane kernels
-  static const bool v = getenv("BLS_PERCALL") && !strcmp(getenv("BLS_PERCALL"), "lane");
-  return v;
-}
-
 int bls_verify(bls_ctx* ctx, const uint8_t* pk48, const uint8_t* msg, size_t msg_len, const uint8_t* sig96) {
   API_ENTER(ctx);
   if (!pk48 || !sig96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
-  if (!percall_lane()) return verify_percall(ctx, pk48, 1, msg, msg_len, sig96);
-  uint8_t* d;
-  int* d_r;
-  SCR(S_IN0, 48 + 96 + msg_len, d);
-  SCR(S_INT, 4, d_r);
-  CK(h2d(ctx, d, pk48, 48));
-  CK(h2d(ctx, d + 48, sig96, 96));
-  CK(h2d(ctx, d + 144, msg, msg_len));
-  LK(launch_verify_single(ctx->j->stream, d, d + 144, (uint32_t)msg_len, d + 48, d_r));
-  int r = 0;
-  CK(d2h(ctx, &r, d_r, sizeof r));
-  return r ? 1 : 0;
+  return verify_percall(ctx, pk48, 1, msg, msg_len, sig96);
 }
 
 int bls_fast_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
@@ -493,25 +475,7 @@ int bls_fast_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, cons
   API_ENTER(ctx);
   if ((!pks48 && n) || !sig96 || (!msg && msg_len) || msg_len > 0xffffffffu) return BLS_E_ARG;
   if (n == 0) return 0;
-  if (!percall_lane()) return verify_percall(ctx, pks48, n, msg, msg_len, sig96);
-  G1A* a;
-  int* ok;
-  int v = validate_pks(ctx, pks48, n, &a, &ok);
-  if (v <= 0) return v;
-  G1J *tmp, *apk;
-  uint8_t* d;
-  int* d_r;
-  SCR(S_G1J_T, 1024, tmp);
-  SCR(S_G1J, 1, apk);
-  SCR(S_IN1, 96 + msg_len, d);
-  SCR(S_INT, 4, d_r);
-  LK(launch_g1_sum_aff(ctx->j->stream, a, nullptr, n, tmp, apk));
-  CK(h2d(ctx, d, sig96, 96));
-  CK(h2d(ctx, d + 96, msg, msg_len));
-  LK(launch_verify_apk(ctx->j->stream, apk, d + 96, (uint32_t)msg_len, d, d_r));
-  int r = 0;
-  CK(d2h(ctx, &r, d_r, sizeof r));
-  return r ? 1 : 0;
+  return verify_percall(ctx, pks48, n, msg, msg_len, sig96);
 }
 
 int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msgs, const size_t* msg_lens,
@@ -551,13 +515,11 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
   {
-    Fp* d_u;
     Fd* d_hf;
     int* d_flag;
-    SCR(S_AV_U, 8 * n, d_u);
     SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
     SCR(S_AV_FLAG, n, d_flag);
-    LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_u, d_hf, Q, d_flag));
+    LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_hf, Q, d_flag));
     CK(h2c_fallback(ctx, ctx->j->stream, n, d_msgs, d_offs, d_flag, Q));
   }
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->j->stream, P + n);
@@ -837,7 +799,6 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   G1A* rP;
   G2A *sig, *H, *saff;
   Fp12 *f, *ft, *fo;
-  Fp* U;
   Fd *msmf, *hcf;
   uint64_t* rsc;
   uint32_t* msmu;
@@ -848,26 +809,16 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_SIG, B, sig);
   SCR(S_RP, B + 1, rP);
   SCR(S_H, B, H);
-  SCR(S_U, 8 * B, U);
   SCR(S_FLAG, B, flag);
   SCR(S_RSC, B, rsc);
   SCR(S_MSMU, msm_scratch_u32(B), msmu);
   SCR(S_MSMF, msm_scratch_fd(), msmf);
   SCR(S_HCF, h2c_scratch_fd(B), hcf);
   SCR(S_RPJ, B, rpj);
-  // Miller loop of (r_i apk_i, H_i): split (G2 lines on stream2 right after
-  // hash_to_G2, f accumulation on stream1) unless BLS_ML_MODE=fused / st1
-  // 5 (default): lines on stream2, f accumulated by k_miller_acc4<2> (four lanes per f, two pairs per f:
-  // one squaring per step for both; measured 1.31M FAV/s against 1.29M for acc4 and 1.16M for acc2);
-  // A/B knobs: BLS_ML_MODE=acc4 (four lanes, one pair per f), acc2 (k_miller_acc2, two lanes per pair),
-  // acc1 (k_miller_acc, one lane per pair), st1 (both on stream1), fused (k_miller_lane), acc4g4 (four pairs per f)
-  static const int ml_mode = [] {
-    const char* m = getenv("BLS_ML_MODE");
-    return !m ? 5 : !strcmp(m, "fused") ? 0 : !strcmp(m, "st1") ? 1 : !strcmp(m, "acc1") ? 2 : !strcmp(m, "acc2") ? 3
-                  : !strcmp(m, "acc4") ? 4 : !strcmp(m, "acc4g4") ? 6 : 5;
-  }();
-  uint32_t* mlines = nullptr;
-  if (ml_mode) SCR(S_MLINES, miller_lines_u32(B), mlines);
+  // Miller loop of (r_i apk_i, H_i), split: G2 lines (k_miller_lines2) on stream2 right after hash_to_G2, f
+  // accumulated on stream1 by k_miller_acc4<2> (four lanes per f, two pairs per f: one squaring per step for both)
+  uint32_t* mlines;
+  SCR(S_MLINES, miller_lines_u32(B), mlines);
   SCR(S_SAFF, 1, saff);
   SCR(S_MSTAT, B, dstat);
   SCR(S_F, B + 2, f);
@@ -876,8 +827,6 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_SEED, 32, d_seed);
   CK(h2d(ctx, d_seed, seed32, 32));
   hipStream_t st = ctx->j->stream, st2 = ctx->j->stream2, st3 = ctx->j->stream3;
-  static const bool serial = getenv("BLS_SERIAL") != nullptr;  // profiling knob: one stream, no overlap
-  if (serial) st2 = st3 = st;
   // Three branches:
   //   stream1: registry gather (affine apk) -> subgroup / r_i apk_i chains -> Miller loops
   //   stream2: hash_to_G2 of every message
@@ -886,9 +835,9 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   HIPCK(hipEventRecord(ctx->j->ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, ctx->j->ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_fork, 0));
-  PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, U, hcf, H, flag));
+  PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, hcf, H, flag));
   CK(h2c_fallback(ctx, st2, B, d_msgs, nullptr, flag, H));
-  if (ml_mode >= 2) PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
+  PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
   HIPCK(hipEventRecord(ctx->j->ev_join, st2));
   PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
   HIPCK(hipEventRecord(ctx->j->ev_sig, st3));
@@ -913,25 +862,8 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   PROF(10, launch_sig_vm(st, B, gstat, status, dstat, apka, sig, rsc, rpj, rP));
   // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_join, 0));
-  static const bool ml_vm = getenv("BLS_ML_VM") != nullptr;  // A/B knob: wave-program Miller (2 pairs per f)
-  if (ml_vm) {
-    PROF(5, launch_miller2(st, rP, H, status, B, f));
-    PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
-  } else {
-    if (ml_mode == 1) PROF(12, launch_miller_lines(st, H, B, mlines));
-    size_t nf = B;  // Miller values to multiply
-    if (ml_mode >= 4) {
-      const int G = ml_mode == 6 ? 4 : ml_mode == 5 ? 2 : 1;
-      PROF(5, launch_miller_acc4(st, rP, H, status, B, mlines, f, G));
-      nf = (B + G - 1) / G;
-    } else if (ml_mode == 3)
-      PROF(5, launch_miller_acc2(st, rP, H, status, B, mlines, f));
-    else if (ml_mode)
-      PROF(5, launch_miller_acc(st, rP, H, status, B, mlines, f));
-    else
-      PROF(5, launch_miller_lane(st, rP, H, status, B, f));
-    PROF(6, launch_fp12_prod_vm(st, f, nf, ft, f + B));
-  }
+  PROF(5, launch_miller_acc4(st, rP, H, status, B, mlines, f, 2));
+  PROF(6, launch_fp12_prod_vm(st, f, (B + 1) / 2, ft, f + B));
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_msm, 0));
   LK(launch_fp12_prod_vm(st, f + B, 2, ft, fo));
   ctx->j->fav_B = B;
@@ -1168,14 +1100,12 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
   SCR(S_FPART, 1, fo);
   LK(launch_key_validate(st, d_pk, total, d_pa, d_pok));
   LK(launch_sig_validate(st, d_sig, B, d_sa, d_sok));
-  {  // hash_to_G2 of every message: lane SSWU + VM isogeny / cofactor clearing (as in the FAV batch)
-    Fp* d_u;
+  {  // hash_to_G2 of every message (as in the FAV batch)
     Fd* d_hf;
     int* d_flag;
-    SCR(S_AV_U, 8 * total, d_u);
     SCR(S_AV_HCF, h2c_scratch_fd(total), d_hf);
     SCR(S_AV_FLAG, total, d_flag);
-    LK(launch_h2c_msgs(st, total, d_msgs, d_moffs, d_u, d_hf, d_h, d_flag));
+    LK(launch_h2c_msgs(st, total, d_msgs, d_moffs, d_hf, d_h, d_flag));
     CK(h2c_fallback(ctx, st, total, d_msgs, d_moffs, d_flag, d_h));
   }
   LK(launch_av_items(st, B, d_io, d_pok, d_sok, d_sa, d_rsc, d_status, P2, Q2));

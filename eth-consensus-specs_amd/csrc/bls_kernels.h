@@ -10,8 +10,6 @@ hipError_t launch_g1_sum_aff(hipStream_t st, const G1A* in, const int* ok, size_
 hipError_t launch_g2_sum_aff(hipStream_t st, const G2A* in, const int* ok, size_t n, G2J* tmp, G2J* out);
 hipError_t launch_g1_compress(hipStream_t st, const G1J* in, uint8_t* out48, int* is_inf);
 hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96);
-hipError_t launch_verify_single(hipStream_t st, const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig, int* out);
-hipError_t launch_verify_apk(hipStream_t st, const G1J* apk, const uint8_t* msg, uint32_t len, const uint8_t* sig, int* out);
 hipError_t launch_percall_pairs(hipStream_t st, const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum,
                                 const int* sig_ok, G1A* P, int* live);
 hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst, uint32_t dst_len, G2A* out);
@@ -44,13 +42,11 @@ constexpr int HCF = 24;  // hash_to_G2 staging: Fd slots per item (bls_fav_kerne
 // gstat: gather status (read-only: the MSM reads it concurrently on another stream); status: written
 hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
                            const G2A* sig, const uint64_t* rsc, G1P* rPj);
-hipError_t launch_g2x_lane(hipStream_t st, size_t B, Fd* hf, int src, int dst);
 // hf: h2c_scratch_fd(B) Fd slots of staging between the hash_to_G2 phases
 size_t h2c_scratch_fd(size_t B);
-hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fp* U, Fd* hf, G2A* H,
-                      int* flag);
+hipError_t launch_h2c(hipStream_t st, size_t B, const uint8_t* msgs32, const int* status, Fd* hf, G2A* H, int* flag);
 // hash_to_G2 (POP DST) of B messages of any length, msgs[offs[i] .. offs[i+1]); same phases as launch_h2c
-hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fp* U, Fd* hf, G2A* H,
+hipError_t launch_h2c_msgs(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, Fd* hf, G2A* H,
                            int* flag);
 // exceptional h2c items (flag set: an isogeny denominator vanished) recomputed by one workgroup; offs == nullptr
 // for 32-byte messages.  Not part of launch_h2c / launch_h2c_msgs: the caller picks its stream (bls_capi.hip).
@@ -63,17 +59,10 @@ hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status
 size_t msm_scratch_u32(size_t B);
 size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
-// one lane per pair (bls_miller_lane.hip): f[i] = Miller value of pair i (1 if skipped)
-hipError_t launch_miller_lane(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 // the same Miller values in two kernels (G2 lines, then f); L: miller_lines_u32(n) words of scratch
 constexpr int MILLER_NLINES = 68;  // 63 doublings + 5 additions (|x| = 0xd201000000010000)
 size_t miller_lines_u32(size_t n);
 hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L);
-hipError_t launch_miller_acc(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
-                             Fp12* f);
-// the same f accumulation with two lanes per pair (bls_miller_pair.hip): f.c0 / f.c1 on lanes 2k / 2k+1
-hipError_t launch_miller_acc2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
-                              Fp12* f);
 // four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values
 hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                               Fp12* f, int G);

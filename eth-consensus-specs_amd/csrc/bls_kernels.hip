@@ -97,29 +97,6 @@ __global__ void k_g2_compress(const G2J* in, uint8_t* out96) {
   g2_compress(out96, jac_to_aff(in[0]));
 }
 
-// ------------------------------------------------------------ per-call ---
-__global__ void k_verify_single(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
-                                int* out) {
-  if (threadIdx.x || blockIdx.x) return;
-  G1A pk;
-  if (!key_validate(pk, pk48)) {
-    *out = 0;
-    return;
-  }
-  *out = core_verify_point(pk, msg, msg_len, DST_POP_DEV, 43, sig96);
-}
-
-// CoreVerify on an aggregate (Jacobian) public key; identity -> invalid.
-__global__ void k_verify_apk(const G1J* apk, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96, int* out) {
-  if (threadIdx.x || blockIdx.x) return;
-  G1A a = jac_to_aff(apk[0]);
-  if (a.inf) {
-    *out = 0;
-    return;
-  }
-  *out = core_verify_point(a, msg, msg_len, DST_POP_DEV, 43, sig96);
-}
-
 // Per-call path (bls_verify / bls_fast_aggregate_verify): the pairs
 // (apk, H(m)) and (-G1, sigma) for k_miller2_vm.  apk is the validated key
 // (n == 1) or the sum of the validated keys; *live = 0 if any key failed
@@ -195,115 +172,14 @@ __global__ void __launch_bounds__(64) k_sk_to_pk_many(const uint8_t* sks32, size
 }
 
 // ------------------------------------------------------- FAV batch path --
-// (1) aggregate pubkeys: one 64-lane workgroup per item.  Each lane adds its
-//     strided share of the registry points with the complete projective
-//     mixed addition (Renes-Costello-Batina alg. 8, 11 products, no
-//     exceptional cases), then an LDS tree of complete additions (alg. 7).
-BLS_HD Fp fp_x12(const Fp& a) {  // 3b * a, b = 4
-  const Fp a2 = fp_dbl(a), a4 = fp_dbl(a2);
-  return fp_add(fp_dbl(a4), a4);
-}
-
-// Inlined products: this is the gather's inner loop (32 mixed additions per lane at
-// n = 512); out-of-line calls cost ~40 % of the mad rate at this occupancy
-// (profiles/r01_s2_fmerate_microbench.txt) and their frames were the kernel's scratch.
-__device__ __forceinline__ G1P g1p_add_aff(const G1P& p, const Fp& x2, const Fp& y2) {
-  Fp t0 = fp_mul_i(p.x, x2);
-  Fp t1 = fp_mul_i(p.y, y2);
-  Fp t3 = fp_sub(fp_sub(fp_mul_i(fp_add(x2, y2), fp_add(p.x, p.y)), t0), t1);
-  const Fp t4 = fp_add(fp_mul_i(y2, p.z), p.y);
-  Fp y3 = fp_add(fp_mul_i(x2, p.z), p.x);
-  t0 = fp_add(fp_dbl(t0), t0);
-  const Fp t2 = fp_x12(p.z);
-  Fp z3 = fp_add(t1, t2);
-  t1 = fp_sub(t1, t2);
-  y3 = fp_x12(y3);
-  G1P r;
-  r.x = fp_sub(fp_mul_i(t3, t1), fp_mul_i(t4, y3));
-  r.y = fp_add(fp_mul_i(t1, z3), fp_mul_i(y3, t0));
-  r.z = fp_add(fp_mul_i(z3, t4), fp_mul_i(t0, t3));
-  return r;
-}
-
-__device__ __forceinline__ G1P g1p_add(const G1P& p, const G1P& q) {
-  Fp t0 = fp_mul_v(p.x, q.x);
-  Fp t1 = fp_mul_v(p.y, q.y);
-  Fp t2 = fp_mul_v(p.z, q.z);
-  const Fp t3 = fp_sub(fp_sub(fp_mul_v(fp_add(p.x, p.y), fp_add(q.x, q.y)), t0), t1);
-  const Fp t4 = fp_sub(fp_sub(fp_mul_v(fp_add(p.y, p.z), fp_add(q.y, q.z)), t1), t2);
-  Fp y3 = fp_sub(fp_sub(fp_mul_v(fp_add(p.x, p.z), fp_add(q.x, q.z)), t0), t2);
-  t0 = fp_add(fp_dbl(t0), t0);
-  t2 = fp_x12(t2);
-  Fp z3 = fp_add(t1, t2);
-  t1 = fp_sub(t1, t2);
-  y3 = fp_x12(y3);
-  G1P r;
-  r.x = fp_sub(fp_mul_v(t3, t1), fp_mul_v(t4, y3));
-  r.y = fp_add(fp_mul_v(t1, z3), fp_mul_v(y3, t0));
-  r.z = fp_add(fp_mul_v(z3, t4), fp_mul_v(t0, t3));
-  return r;
-}
-
-// L lanes per aggregate, 64 / L aggregates per workgroup.  The LDS tree
-// costs log2(L) full additions of the whole wave, so for mainnet-sized
-// committees L = 16 (32 mixed additions per lane + 4 tree levels) beats 64
-// lanes (8 + 6 levels: the tree was ~45 % of the wave's time).
-template <int L>
-__global__ void __launch_bounds__(64) k_fav_gather(const uint32_t* idx, const uint64_t* offs, size_t B,
-                                                   const RegKey* reg, uint32_t reg_n, G1P* apk, int* status) {
-  constexpr int IPW = 64 / L;
-  __shared__ G1P sh[64];
-  __shared__ int bad[IPW];
-  const int sub = (int)threadIdx.x / L, ln = (int)threadIdx.x % L;
-  const size_t b = (size_t)blockIdx.x * IPW + sub;
-  if ((int)threadIdx.x < IPW) bad[threadIdx.x] = 0;
-  __syncthreads();
-  G1P acc{fp_zero(), FP_ONE, fp_zero()};  // identity (0 : 1 : 0)
-  int mybad = 0;
-  uint64_t lo = 0, hi = 0;
-  if (b < B) {
-    lo = offs[b];
-    hi = offs[b + 1];
-    for (uint64_t j = lo + ln; j < hi; j += L) {
-      const uint32_t k = idx[j];
-      if (k >= reg_n) {
-        mybad = 1;
-        continue;
-      }
-      // one 96-B record: six 16-B loads, x's top bit is the validity flag
-      const uint4* r = reinterpret_cast<const uint4*>(reg + k);
-      Fp x, y;
-      uint4* xv = reinterpret_cast<uint4*>(x.l);
-      uint4* yv = reinterpret_cast<uint4*>(y.l);
-      xv[0] = r[0];
-      xv[1] = r[1];
-      xv[2] = r[2];
-      yv[0] = r[3];
-      yv[1] = r[4];
-      yv[2] = r[5];
-      if (!(x.l[11] & REG_VALID)) {
-        mybad = 1;
-      } else {
-        x.l[11] &= ~REG_VALID;
-        acc = g1p_add_aff(acc, x, y);
-      }
-    }
-  }
-  if (mybad) atomicOr(&bad[sub], 1);
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-#pragma unroll 1
-  for (int s = L / 2; s > 0; s >>= 1) {
-    if (ln < s) sh[threadIdx.x] = g1p_add(sh[threadIdx.x], sh[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (ln == 0 && b < B) {  // projective aggregate key; the identity is invalid (KeyValidate of the sum)
-    apk[b] = sh[threadIdx.x];
-    status[b] = (hi > lo && !bad[sub] && !fp_is_zero(sh[threadIdx.x].z)) ? 1 : 0;
-  }
-}
-
-// The same gather in the redundant digit form: bls_fq_g1.h (g1q_add_aff, g1q_add).
+// Aggregate pubkeys: L lanes per aggregate, 64 / L aggregates per workgroup.
+// Each lane adds its strided share of the registry points with the complete
+// projective mixed addition (Renes-Costello-Batina alg. 8, 11 products, no
+// exceptional cases), then an LDS tree of complete additions (alg. 7), all in
+// the redundant digit form (bls_fq_g1.h: g1q_add_aff, g1q_add).  The tree costs
+// log2(L) full additions of the whole wave, so for mainnet-sized committees
+// L = 16 (32 mixed additions per lane + 4 tree levels) beats 64 lanes (8 + 6
+// levels: the tree was ~45 % of the wave's time).
 template <int L>
 __global__ void __launch_bounds__(64) k_fav_gather_q(const uint32_t* idx, const uint64_t* offs, size_t B,
                                                      const RegKey* reg, uint32_t reg_n, G1P* apk, int* status) {
@@ -585,16 +461,6 @@ hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96) {
   LAUNCH(k_g2_compress, 1, 64, st, in, out96);
   return hipSuccess;
 }
-hipError_t launch_verify_single(hipStream_t st, const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig,
-                                int* out) {
-  LAUNCH(k_verify_single, 1, 64, st, pk, msg, len, sig, out);
-  return hipSuccess;
-}
-hipError_t launch_verify_apk(hipStream_t st, const G1J* apk, const uint8_t* msg, uint32_t len, const uint8_t* sig,
-                             int* out) {
-  LAUNCH(k_verify_apk, 1, 64, st, apk, msg, len, sig, out);
-  return hipSuccess;
-}
 hipError_t launch_percall_pairs(hipStream_t st, const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum,
                                 const int* sig_ok, G1A* P, int* live) {
   LAUNCH(k_percall_pairs, 1, 64, st, keys, key_ok, n, apk_sum, sig_ok, P, live);
@@ -622,22 +488,10 @@ hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t
   if (!B) return hipSuccess;
   // lanes per aggregate: 16 while that still gives >= ~2 waves per SIMD and the
   // committees are not huge (the per-lane chains stay short), else 64
-  static const int forced = getenv("BLS_GATHER_L") ? atoi(getenv("BLS_GATHER_L")) : 0;
-  int L = forced ? forced : (B >= 8192 ? 16 : 64);
-  // A/B knob: BLS_GATHER_PACKED=1 runs the packed-Fp gather (k_fav_gather)
-  static const bool packed = getenv("BLS_GATHER_PACKED") != nullptr;
-  if (!packed && L == 16)
+  if (B >= 8192)
     LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
-  else if (!packed && L == 64)
-    LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
-  else if (L == 16)
-    LAUNCH(k_fav_gather<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
-  else if (L == 8)
-    LAUNCH(k_fav_gather<8>, (unsigned)((B + 7) / 8), 64, st, idx, offs, B, reg, reg_n, apk, status);
-  else if (L == 32)
-    LAUNCH(k_fav_gather<32>, (unsigned)((B + 1) / 2), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else
-    LAUNCH(k_fav_gather<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
+    LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
   return hipSuccess;
 }
 hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP,

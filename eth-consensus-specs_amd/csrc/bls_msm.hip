@@ -2,9 +2,8 @@
 //
 // The 64-bit scalars split into 8 windows; the (item, window) pairs with a
 // nonzero digit d are counting-sorted into 8 x 255 buckets (atomic histogram,
-// one prefix pass, atomic scatter), and each bucket's points are added on the
-// VM (4 buckets per workgroup, one mixed addition per step, select for
-// buckets that ran out of points).  The bucket reduction is parallel:
+// one prefix pass, atomic scatter), and each bucket's points are added by a
+// lane pair (k_msm_bucket2, one mixed addition per step).  The bucket reduction is parallel:
 //   U_b = sum_{d : bit k of d} B_{w,d}   (b = 8w + k; 64 sums of 128 buckets,
 //                                          a 7-level pairwise tree), then
 //   S   = sum_b 2^b U_b                   (a 6-level tree of A + [2^k] B).
@@ -20,7 +19,6 @@
 namespace bls {
 
 constexpr int MSM_W = 8, MSM_NB = MSM_W * 256;
-constexpr int MSM_G = 4;  // buckets per workgroup
 
 // cnt[MSM_NB] must be zero on entry.
 __global__ void __launch_bounds__(256) k_msm_count(size_t B, const int* status, const int* status2, const uint64_t* rsc,
@@ -57,53 +55,6 @@ __global__ void __launch_bounds__(256) k_msm_scatter(size_t B, const int* status
   if (d) lst[atomicAdd(&cur[w * 256 + d], 1u)] = (uint32_t)i;
 }
 
-// Bucket sums: bucket b = w * 256 + d; bsum[b] = (X : Y : Z) projective.
-template <int G>
-__global__ void __launch_bounds__(64) k_msm_bucket(const uint32_t* off, const uint32_t* lst, const G2A* sig,
-                                                  Fd* bsum) {
-  __shared__ Fd s[WP_NCONST + G * WL_MB_STRIDE];
-  __shared__ uint32_t pred[G];
-  __shared__ uint32_t lo[G], len[G];
-  __shared__ uint32_t maxlen;
-  const int lane = threadIdx.x;
-  const int b0 = blockIdx.x * G;
-  vm_load_consts(s);
-  if (lane == 0) maxlen = 0;
-  __syncthreads();
-  if (lane < G) {
-    lo[lane] = off[b0 + lane];
-    len[lane] = off[b0 + lane + 1] - lo[lane];
-    atomicMax(&maxlen, len[lane]);
-  }
-  const int item0 = WP_NCONST;
-  for (int k = lane; k < 6 * G; k += 64) {  // R = (0 : 1 : 0)
-    const int g = k / 6, j = k % 6;
-    Fd v = fd_zero();
-    if (j == 2) v = fd_from_fp(FP_ONE);
-    s[item0 + g * WL_MB_STRIDE + WL_MB_R + j] = v;
-  }
-  __syncthreads();
-  const uint32_t steps = maxlen;
-  for (uint32_t t = 0; t < steps; t++) {
-    for (int k = lane; k < 4 * G; k += 64) {
-      const int g = k >> 2, j = k & 3;
-      Fp v = fp_zero();
-      if (t < len[g]) {
-        const G2A& q = sig[lst[lo[g] + t]];
-        v = j == 0 ? q.x.c0 : (j == 1 ? q.x.c1 : (j == 2 ? q.y.c0 : q.y.c1));
-      }
-      s[item0 + g * WL_MB_STRIDE + WL_MB_Q + j] = fd_from_fp(v);
-    }
-    if (lane < G) pred[lane] = t < len[lane] ? 1u : 0u;
-    __syncthreads();
-    vm_run<G>(VM_PROG(MB_ADD), s, item0, WL_MB_STRIDE, pred);
-  }
-  for (int k = lane; k < 6 * G; k += 64) {
-    const int g = k / 6, j = k % 6;
-    bsum[(size_t)(b0 + g) * 6 + j] = s[item0 + g * WL_MB_STRIDE + WL_MB_R + j];
-  }
-}
-
 // U-tree input: ubase[(8w + k) * 128 + j] = B_{w, d_j} with d_j the j-th digit
 // having bit k set (bit k inserted into j).
 __global__ void __launch_bounds__(256) k_msm_gather_bits(const Fd* bsum, Fd* ubase) {
@@ -113,35 +64,6 @@ __global__ void __launch_bounds__(256) k_msm_gather_bits(const Fd* bsum, Fd* uba
   const int w = b >> 3, k = b & 7;
   const int d = ((j >> k) << (k + 1)) | (1 << k) | (j & ((1 << k) - 1));
   ubase[t] = bsum[(size_t)(w * 256 + d) * 6 + c];
-}
-
-// One tree level: out[j] = in[2j] + [2^k] in[2j+1] (k = 0: plain sum).
-template <int G>
-__global__ void __launch_bounds__(64) k_msm_tree(const Fd* in, int nout, int k, Fd* out) {
-  __shared__ Fd s[WP_NCONST + G * WL_MT_STRIDE];
-  const int lane = threadIdx.x;
-  const int j0 = blockIdx.x * G;
-  vm_load_consts(s);
-  const int item0 = WP_NCONST;
-  for (int q = lane; q < 12 * G; q += 64) {
-    const int g = q / 12, c = q % 12;
-    const int j = j0 + g < nout ? j0 + g : nout - 1;
-    s[item0 + g * WL_MT_STRIDE + WL_MT_A + c] = in[(size_t)(2 * j) * 6 + c];  // A then B (contiguous)
-  }
-  __syncthreads();
-  switch (k) {
-    case 0: vm_run<G>(VM_PROG(MT_ADD), s, item0, WL_MT_STRIDE, nullptr); break;
-    case 1: vm_run<G>(VM_PROG(MT_P1), s, item0, WL_MT_STRIDE, nullptr); break;
-    case 2: vm_run<G>(VM_PROG(MT_P2), s, item0, WL_MT_STRIDE, nullptr); break;
-    case 4: vm_run<G>(VM_PROG(MT_P4), s, item0, WL_MT_STRIDE, nullptr); break;
-    case 8: vm_run<G>(VM_PROG(MT_P8), s, item0, WL_MT_STRIDE, nullptr); break;
-    case 16: vm_run<G>(VM_PROG(MT_P16), s, item0, WL_MT_STRIDE, nullptr); break;
-    default: vm_run<G>(VM_PROG(MT_P32), s, item0, WL_MT_STRIDE, nullptr); break;
-  }
-  for (int q = lane; q < 6 * G; q += 64) {
-    const int g = q / 6, c = q % 6;
-    if (j0 + g < nout) out[(size_t)(j0 + g) * 6 + c] = s[item0 + g * WL_MT_STRIDE + WL_MT_O + c];
-  }
 }
 
 // ----------------------------------------------------------- lane form --
@@ -249,12 +171,7 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
     hipLaunchKernelGGL(k_msm_scatter, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cur, lst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // A/B knob: BLS_MSM_VM=1 runs the bucket sums and trees as wave programs (k_msm_bucket<4>, k_msm_tree<4>)
-  static const bool vm = getenv("BLS_MSM_VM") != nullptr;
-  if (vm)
-    hipLaunchKernelGGL(k_msm_bucket<MSM_G>, dim3(MSM_NB / MSM_G), dim3(64), 0, st, off, lst, sig, bsum);
-  else
-    hipLaunchKernelGGL(k_msm_bucket2, dim3(2 * MSM_NB / 64), dim3(64), 0, st, off, lst, sig, bsum);
+  hipLaunchKernelGGL(k_msm_bucket2, dim3(2 * MSM_NB / 64), dim3(64), 0, st, off, lst, sig, bsum);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_gather_bits, dim3(64 * 128 * 6 / 256), dim3(256), 0, st, bsum, ping);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -262,10 +179,7 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   Fd* a = ping;
   Fd* b = pong;
   for (int n = 64 * 64; n >= 64; n >>= 1) {
-    if (vm)
-      hipLaunchKernelGGL(k_msm_tree<4>, dim3((n + 3) / 4), dim3(64), 0, st, a, n, 0, b);
-    else
-      hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, 0, b);
+    hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, 0, b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     Fd* t = a;
     a = b;
@@ -274,10 +188,7 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   // weighted tree: sum_b 2^b U_b, 64 -> 1
   int k = 1;
   for (int n = 32; n >= 1; n >>= 1, k <<= 1) {
-    if (vm)
-      hipLaunchKernelGGL(k_msm_tree<4>, dim3((n + 3) / 4), dim3(64), 0, st, a, n, k, b);
-    else
-      hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, k, b);
+    hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, k, b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     Fd* t = a;
     a = b;

@@ -4,8 +4,6 @@
 #include "bls_kernels.h"
 #include "bls_vm.h"
 
-#include <stdlib.h>
-
 namespace bls {
 
 // ---- slot <-> Fp12 (w-basis order: slot 2k = Re c_k, 2k+1 = Im c_k) ----
@@ -261,20 +259,9 @@ hipError_t launch_fp12_seg_prod(hipStream_t st, const Fp12* in, const uint64_t* 
   return hipGetLastError();
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
 hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
   if (!n) return hipSuccess;
-  static const int g = env_int("BLS_ML_G", ML_G);  // tuning knob (pairs per workgroup)
-  if (g == 1)
-    hipLaunchKernelGGL(k_miller_vm<1>, dim3((unsigned)n), dim3(64), 0, st, P, Q, ok, n, f);
-  else if (g == 4)
-    hipLaunchKernelGGL(k_miller_vm<4>, dim3((unsigned)((n + 3) / 4)), dim3(64), 0, st, P, Q, ok, n, f);
-  else
-    hipLaunchKernelGGL(k_miller_vm<2>, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, P, Q, ok, n, f);
+  hipLaunchKernelGGL(k_miller_vm<ML_G>, dim3((unsigned)((n + ML_G - 1) / ML_G)), dim3(64), 0, st, P, Q, ok, n, f);
   return hipGetLastError();
 }
 
@@ -283,11 +270,7 @@ hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const 
 hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
   if (!n) return hipSuccess;
   const size_t ngrp = (n + 1) / 2;
-  static const int g = env_int("BLS_M2_G", 2);  // tuning knob: groups per workgroup
-  if (g == 1)
-    hipLaunchKernelGGL(k_miller2_vm<1>, dim3((unsigned)ngrp), dim3(64), 0, st, P, Q, ok, n, f);
-  else
-    hipLaunchKernelGGL(k_miller2_vm<2>, dim3((unsigned)((ngrp + 1) / 2)), dim3(64), 0, st, P, Q, ok, n, f);
+  hipLaunchKernelGGL(k_miller2_vm<2>, dim3((unsigned)((ngrp + 1) / 2)), dim3(64), 0, st, P, Q, ok, n, f);
   return hipGetLastError();
 }
 
