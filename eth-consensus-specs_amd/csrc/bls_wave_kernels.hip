@@ -1,6 +1,6 @@
 // Wave-program kernels (bls_vm.h): Miller loop (G pairs per 64-lane
-// workgroup), chunked Fp12 products, and the final exponentiation of a
-// product of partials (one workgroup).
+// workgroup) and chunked Fp12 products.  (The final-exponentiation check is
+// k_fe_check, bls_fe.hip.)
 #include "bls_kernels.h"
 #include "bls_vm.h"
 
@@ -131,98 +131,6 @@ __global__ void __launch_bounds__(64) k_miller2_vm(const G1A* P, const G2A* Q, c
   }
 }
 
-// ============================================ Fp12 registers of one item ==
-// Region WL_FE_*: registers R0..R6 (12 slots each) | scratch.  Every
-// operation is a program instance bound to its registers (FE_* in wavec).
-__device__ __forceinline__ Fd* fe_reg(Fd* s, int k) { return s + WP_NCONST + 12 * k; }
-__device__ __forceinline__ void fe_run(Fd* s, const VmProg p) { vm_run<1>(p, s, WP_NCONST, 0, nullptr); }
-__device__ __forceinline__ void fe_copy(Fd* s, int dst, int a) {
-  if (threadIdx.x < 12) fe_reg(s, dst)[threadIdx.x] = fe_reg(s, a)[threadIdx.x];
-  __syncthreads();
-}
-__device__ __forceinline__ void fe_conj(Fd* s, int dst, int a) {
-  if (threadIdx.x < 12) {
-    const Fp v = fp_from_fd(fe_reg(s, a)[threadIdx.x]);
-    fe_reg(s, dst)[threadIdx.x] = fd_from_fp(((threadIdx.x >> 1) & 1) ? fp_neg(v) : v);
-  }
-  __syncthreads();
-}
-// R1 = R2^x (x = -|x|; cyclotomic input, so the inverse is the conjugate)
-__device__ void fe_pow_x(Fd* s) {
-  fe_run(s, VM_PROG(FE_POWX_0));
-  fe_run(s, VM_PROG(FE_POWX_1));
-  fe_run(s, VM_PROG(FE_POWX_2));
-  fe_run(s, VM_PROG(FE_POWX_3));
-  fe_run(s, VM_PROG(FE_POWX_4));
-  fe_run(s, VM_PROG(FE_POWX_5));
-  fe_conj(s, 1, 1);
-}
-
-// Product of n Fp12 values, then the final exponentiation; *out = (result == 1).
-// With sel != nullptr, workgroup b checks the single value fin[sel[b]] and
-// writes out[b] (the batched checks of a bisection round).
-// Easy part (p^6-1)(p^2+1); hard part via (x-1)^2 (x+p) (x^2+p^2-1) + 3, which
-// returns e^3 (e == 1 <=> e^3 == 1 since gcd(3, r) = 1).
-__global__ void __launch_bounds__(64) k_final_check_vm(const Fp12* fin, int n, const uint32_t* sel, int* out) {
-  __shared__ Fd s[WP_NCONST + WL_FE_STRIDE];
-  __shared__ Fp12 inv;
-  __shared__ int okc;
-  const int lane = threadIdx.x;
-  vm_load_consts(s);
-  if (sel) {
-    fin += sel[blockIdx.x];
-    out += blockIdx.x;
-  }
-  load_fp12(fe_reg(s, 0), fin);
-  for (int i = 1; i < n; i++) {
-    load_fp12(fe_reg(s, 1), fin + i);
-    fe_run(s, VM_PROG(FE_MUL_001));
-  }
-  if (lane == 0) {
-    Fp12 f;
-    for (int j = 0; j < 12; j++) fp12_slot_dst(f, j) = fp_from_fd(fe_reg(s, 0)[j]);
-    inv = fp12_inv(f);
-  }
-  __syncthreads();
-  load_fp12(fe_reg(s, 1), &inv);
-  fe_conj(s, 2, 0);
-  fe_run(s, VM_PROG(FE_MUL_021));    // t = conj(f) * f^-1
-  fe_run(s, VM_PROG(FE_FROB2_10));
-  fe_run(s, VM_PROG(FE_MUL_001));    // t = t^(p^2) * t            (R0)
-  // a = t^((x-1)^2)
-  fe_copy(s, 2, 0);
-  fe_pow_x(s);                       // R1 = t^x
-  fe_conj(s, 2, 0);
-  fe_run(s, VM_PROG(FE_MUL_221));    // R2 = a = t^(x-1)
-  fe_pow_x(s);                       // R1 = a^x
-  fe_conj(s, 3, 2);
-  fe_run(s, VM_PROG(FE_MUL_213));    // R2 = a^(x-1)
-  // b = a^(x+p)
-  fe_pow_x(s);                       // R1 = a^x
-  fe_run(s, VM_PROG(FE_FROB1_32));   // R3 = a^p
-  fe_run(s, VM_PROG(FE_MUL_331));    // R3 = b
-  // c = b^(x^2+p^2-1)
-  fe_copy(s, 2, 3);
-  fe_pow_x(s);                       // R1 = b^x
-  fe_copy(s, 2, 1);
-  fe_pow_x(s);                       // R1 = b^(x^2)
-  fe_run(s, VM_PROG(FE_FROB2_43));   // R4 = b^(p^2)
-  fe_run(s, VM_PROG(FE_MUL_114));
-  fe_conj(s, 4, 3);
-  fe_run(s, VM_PROG(FE_MUL_114));    // R1 = c
-  fe_run(s, VM_PROG(FE_CUBE));       // R5 = t^3
-  fe_run(s, VM_PROG(FE_MUL_115));
-  if (lane == 0) okc = 1;
-  __syncthreads();
-  if (lane < 12) {
-    const Fp v = fp_from_fd(fe_reg(s, 1)[lane]);
-    const bool good = lane == 0 ? fp_is_one(v) : fp_is_zero(v);
-    if (!good) okc = 0;
-  }
-  __syncthreads();
-  if (lane == 0) *out = okc;
-}
-
 // Products of consecutive chunks: out[b] = prod in[b*chunk .. min(n, (b+1)*chunk))
 __global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n, int chunk, Fp12* outp) {
   __shared__ Fd s[WP_NCONST + WL_CH_STRIDE];
@@ -271,17 +179,6 @@ hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int*
   if (!n) return hipSuccess;
   const size_t ngrp = (n + 1) / 2;
   hipLaunchKernelGGL(k_miller2_vm<2>, dim3((unsigned)((ngrp + 1) / 2)), dim3(64), 0, st, P, Q, ok, n, f);
-  return hipGetLastError();
-}
-
-hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out) {
-  hipLaunchKernelGGL(k_final_check_vm, dim3(1), dim3(64), 0, st, f, n, (const uint32_t*)nullptr, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out) {
-  if (!nsel) return hipSuccess;
-  hipLaunchKernelGGL(k_final_check_vm, dim3((unsigned)nsel), dim3(64), 0, st, f, 1, sel, out);
   return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ from oracle import bls_oracle as O
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "hostcheck", f) for f in ("hostcheck.cpp", "hostcheck_fq.cpp", "Makefile")]
+SRCS = [os.path.join(HERE, "hostcheck", f) for f in ("hostcheck.cpp", "hostcheck_fq.cpp", "hostcheck_fe.cpp", "Makefile")]
 LIB = os.path.join(HERE, "hostcheck", "libhostcheck.so")
 INC = os.path.join(ROOT, "eth-consensus-specs_amd", "csrc")
 
@@ -22,7 +22,7 @@ def build(force=False):
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
         return LIB
     # two translation units (the digit-form checks are a long host compile), built in parallel
-    subprocess.check_call(["make", "-j2", "-C", os.path.join(HERE, "hostcheck")], timeout=2400)
+    subprocess.check_call(["make", "-j3", "-C", os.path.join(HERE, "hostcheck")], timeout=2400)
     return LIB
 
 

@@ -7,6 +7,7 @@
 #include "bls_lane.h"
 #include "bls_tower_inline.h"
 #include "bls_pp_lane.h"
+#include "bls_fp_inv.h"
 #include <string.h>
 using namespace bls;
 
@@ -38,6 +39,7 @@ void hc_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp(o, fp_mu
 void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp(o, fp_add(in_fp(a), in_fp(b))); }
 void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp(o, fp_sub(in_fp(a), in_fp(b))); }
 void hc_fp_inv(const uint8_t* a, uint8_t* o) { out_fp(o, fp_inv(in_fp(a))); }
+void hc_fp_inv_sg(const uint8_t* a, uint8_t* o) { out_fp(o, fp_inv_sg(in_fp(a))); }
 void hc_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { out_fp2(o, fp2_mul(in_fp2(a), in_fp2(b))); }
 void hc_fp2_sqr(const uint8_t* a, uint8_t* o) { out_fp2(o, fp2_sqr(in_fp2(a))); }
 void hc_fp2_inv(const uint8_t* a, uint8_t* o) { out_fp2(o, fp2_inv(in_fp2(a))); }

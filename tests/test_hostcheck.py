@@ -338,3 +338,41 @@ def test_fq_g2_add_exception():
     exc, _ = H.call("hc_fq_j2_dbl_add", H.fp2_b(p[0]) + H.fp2_b(p[1]), H.fp2_b(q[0]) + H.fp2_b(q[1]), out=192,
                     ret=True)
     assert exc == 1
+
+
+def _f12_bytes(f):
+    return b"".join(H.fp_b(f[h][k][part]) for h in range(2) for k in range(3) for part in range(2))
+
+
+def _f12_from_bytes(b):
+    v = [int.from_bytes(b[48 * j: 48 * j + 48], "big") for j in range(12)]
+    return tuple(tuple((v[6 * h + 2 * k], v[6 * h + 2 * k + 1]) for k in range(3)) for h in range(2))
+
+
+def test_fe_lane_schedule():
+    """The lane-parallel final exponentiation (bls_fe.h, the kernel's phase tables and schedule) run on the host
+    with the digit-form column / value checks compiled in: FE(f_1 ... f_n)^3 against the oracle for random
+    Fp12 values, and the check verdict 1 for values the final exponentiation maps to 1 (Fp6 elements)."""
+    for n in (1, 2, 3):
+        fs = [tuple(tuple((rng.randrange(O.P), rng.randrange(O.P)) for _ in range(3)) for _ in range(2))
+              for _ in range(n)]
+        prod = fs[0]
+        for g in fs[1:]:
+            prod = O.f12_mul(prod, g)
+        ok, out = H.call("hc_fe_check", b"".join(_f12_bytes(f) for f in fs), n, out=576, ret=True)
+        fe = O.final_exponentiation(prod)
+        assert _f12_from_bytes(out) == O.f12_mul(O.f12_mul(fe, fe), fe)
+        assert ok == (fe == O.F12_ONE)
+    a = tuple((rng.randrange(O.P), rng.randrange(O.P)) for _ in range(3))
+    ok, _ = H.call("hc_fe_check", _f12_bytes((a, ((0, 0), (0, 0), (0, 0)))), 1, out=576, ret=True)
+    assert ok == 1
+
+
+def test_fp_inv_safegcd():
+    """fp_inv_sg (bls_fp_inv.h, Bernstein-Yang divsteps, 15 x 59 steps) against pow(x, -1, p): random values,
+    the edges 0, 1, 2, p - 1, p - 2 and values with long runs of zero / one bits."""
+    vals = [0, 1, 2, O.P - 1, O.P - 2, (1 << 380) - 1, 1 << 380, (O.P - 1) // 2, 3 << 300]
+    vals += [rng.randrange(O.P) for _ in range(300)]
+    for v in vals:
+        out = H.call("hc_fp_inv_sg", H.fp_b(v), out=48)
+        assert int.from_bytes(out, "big") == (pow(v, -1, O.P) if v else 0), hex(v)
