@@ -76,7 +76,7 @@ SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
 LANE_KERNELS = {"miller": 2, "miller_lines": 2, "sig_vm": 3}
 GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
 # profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
-KERNEL_SYMBOL = {"miller": "k_miller_acc4<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
+KERNEL_SYMBOL = {"miller": "k_miller_acc4q<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 LIB = os.path.join(ROOT, "eth-consensus-specs_amd", "libblsmi355x.so")
 
@@ -558,7 +558,8 @@ def main():
         try:  # HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE pass (a PMC run cannot be live)
             with open(os.path.join(ROOT, "tools", "pmc_traffic.json")) as fh:
                 tj = json.load(fh)
-            traffic, tsrc = tj["bytes_per_dispatch"].get(dom), tj["source"]
+            if tj.get("lib_sha256_16") == _lib_sha():  # only the profile of this exact build
+                traffic, tsrc = tj["bytes_per_dispatch"].get(dom), tj["source"]
         except (OSError, ValueError, KeyError):
             pass
         roof = {"bound": "valu-int", "kernel": dom, "symbol": KERNEL_SYMBOL.get(dom), "achieved": round(ach, 4),

@@ -50,13 +50,15 @@ struct Fp6 {
 struct Fp12 {
   Fp6 c0, c1;  // c0 + c1 w,  w^2 = v
 };
-// HBM registry entry: affine (x, y) of one key in Montgomery form, 96 B, no
-// padding and no side array.  Bit 31 of x.l[11] lies above the 381-bit
-// residue and holds the KeyValidate verdict (REG_VALID), so the FAV gather
-// fetches exactly the 96 algorithmic bytes per key (3 x 32-B sectors: the
-// records are 32-B aligned because hipMalloc is 256-B aligned and 96 = 3 x 32).
-struct alignas(16) RegKey {
+// HBM registry entry: affine (x, y) of one key in Montgomery form, 96 B of
+// data in a 128-B record, 128-B aligned (hipMalloc is 256-B aligned), so a
+// random key read is exactly one 128-B line: with 96-B records half of them
+// straddled two lines, and the gather moved ~192 B per key (profiles/r03*_pmc_fetch.md).
+// Bit 31 of x.l[11] lies above the 381-bit residue and holds the KeyValidate
+// verdict (REG_VALID), so no side array is read.
+struct alignas(128) RegKey {
   Fp x, y;
+  uint32_t pad[8];
 };
 constexpr uint32_t REG_VALID = 0x80000000u;
 

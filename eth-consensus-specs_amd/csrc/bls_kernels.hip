@@ -196,23 +196,33 @@ __global__ void __launch_bounds__(64) k_fav_gather_q(const uint32_t* idx, const 
   if (b < B) {
     lo = offs[b];
     hi = offs[b + 1];
-    for (uint64_t j = lo + ln; j < hi; j += L) {
-      const uint32_t k = idx[j];
-      if (k >= reg_n) {
-        mybad = 1;
-        continue;
-      }
-      const uint4* r = reinterpret_cast<const uint4*>(reg + k);
+    // software pipeline: the record of key j + L and the index of key j + 2L are in flight while key j is added
+    // (an out-of-range index reads record 0 and is flagged; every load is unconditional)
+    uint64_t j = lo + ln;
+    uint32_t k1 = j < hi ? idx[j] : 0u;
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(reg + (k1 < reg_n ? k1 : 0u));
+    uint4 r[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) r[w] = reinterpret_cast<const uint4*>(rw)[w];
+    uint32_t k2 = j + L < hi ? idx[j + L] : 0u;
+#pragma unroll 1
+    for (; j < hi; j += L) {
+      uint4 cr[6];
+#pragma unroll
+      for (int w = 0; w < 6; ++w) cr[w] = r[w];
+      const uint32_t ck = k1;
+      k1 = k2;
+      const uint4* nr = reinterpret_cast<const uint4*>(reg + (k1 < reg_n ? k1 : 0u));
+#pragma unroll
+      for (int w = 0; w < 6; ++w) r[w] = nr[w];
+      k2 = j + 2 * L < hi ? idx[j + 2 * L] : 0u;
       Fp x, y;
-      uint4* xv = reinterpret_cast<uint4*>(x.l);
-      uint4* yv = reinterpret_cast<uint4*>(y.l);
-      xv[0] = r[0];
-      xv[1] = r[1];
-      xv[2] = r[2];
-      yv[0] = r[3];
-      yv[1] = r[4];
-      yv[2] = r[5];
-      if (!(x.l[11] & REG_VALID)) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        reinterpret_cast<uint4*>(x.l)[w] = cr[w];
+        reinterpret_cast<uint4*>(y.l)[w] = cr[3 + w];
+      }
+      if (ck >= reg_n || !(x.l[11] & REG_VALID)) {
         mybad = 1;
       } else {
         x.l[11] &= ~REG_VALID;

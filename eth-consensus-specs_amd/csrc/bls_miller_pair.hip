@@ -1,5 +1,7 @@
 // f accumulation of the split Miller loop (the G2 side, k_miller_lines2 in
-// bls_miller_lane.hip, writes the line records) with four lanes per f.
+// bls_miller_lane.hip, writes the line records) with four lanes per f, in the
+// bound-typed redundant digit form (bls_fqb.h).
+#include "bls_fqb.h"
 #include "bls_kernels.h"
 #include "bls_tower_inline.h"
 
@@ -8,14 +10,9 @@ namespace bls {
 namespace {
 
 constexpr int ML_WORDS2 = 72;  // line record: three Fp2 (l0, E*ZZ or r, z3*ZZ or z3), as k_miller_lines2 writes
-
-__device__ __forceinline__ Fp sel_fp(bool c, const Fp& a, const Fp& b) { return fp_select(c, a, b); }
-__device__ __forceinline__ Fp2 sel_fp2(bool c, const Fp2& a, const Fp2& b) {
-  return Fp2{sel_fp(c, a.c0, b.c0), sel_fp(c, a.c1, b.c1)};
-}
-__device__ __forceinline__ Fp6 sel_fp6(bool c, const Fp6& a, const Fp6& b) {
-  return Fp6{sel_fp2(c, a.c0, b.c0), sel_fp2(c, a.c1, b.c1), sel_fp2(c, a.c2, b.c2)};
-}
+// loop-carried bound of the digit-form f halves: value < ML_QF_V p, digits <= ML_QF_D (every step's output is
+// relaxed to it at compile time: qq_sqr ends below 211 p, qq_line below ML_QF_V p)
+constexpr uint64_t ML_QF_V = 256, ML_QF_D = 0x20000000ull + 64;
 
 __device__ __forceinline__ Fp2 ml_load2(const uint32_t* L, size_t n, int w0) {
   Fp2 a;
@@ -27,14 +24,16 @@ __device__ __forceinline__ Fp2 ml_load2(const uint32_t* L, size_t n, int w0) {
   return a;
 }
 
-// The Fp2 products of each Fp6 product run one after another (sched_barrier):
-// each lazy Fp2 product already has three independent mad chains; letting the
-// scheduler interleave six of them held ~6 x 140 registers live and spilled
-// (measured 5.0 ms per 10,000 pairs against 5.7 ms interleaved).
+// The Fp2 products of each Fp6 product run one after another (sched_barrier): letting the scheduler
+// interleave them held too many products live and spilled (the packed-form kernel measured 5.0 ms per
+// 10,000 pairs sequenced against 5.7 ms interleaved).
 #define SEQ() __builtin_amdgcn_sched_barrier(0)
 
-__device__ __forceinline__ Fp6 f6add_raw(const Fp6& a, const Fp6& b) {
-  return Fp6{f2add_raw(a.c0, b.c0), f2add_raw(a.c1, b.c1), f2add_raw(a.c2, b.c2)};
+__device__ __forceinline__ uint32_t dpp_q(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_h(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
 }
 
 }  // namespace
@@ -59,101 +58,125 @@ __device__ __forceinline__ Fp6 f6add_raw(const Fp6& a, const Fp6& b) {
 // shared-squaring model.  The output is one Fp12 per group; the batch product
 // over groups equals the product over pairs, so the verdict and every
 // downstream value are unchanged.
+//
+// f's halves stay in 14 redundant radix-2^29 digits for the whole loop:
+// additions and subtractions are digit-wise (no carry chains, no conditional
+// subtractions) and no product unpacks or repacks its operands (the packed
+// 12-limb kernel this replaces: 4.39 -> 3.68 ms per 10,000 pairs).  Every
+// digit and value bound is checked at compile time (bls_fqb.h).
 namespace {
 
-__device__ __forceinline__ uint32_t dpp_q(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ uint32_t dpp_h(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-}
-__device__ __forceinline__ Fp q_fp(const Fp& a) {
-  Fp r;
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ FqB<V, D> dq(const FqB<V, D>& a) {
+  Fq r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.l[i] = dpp_q(a.l[i]);
-  return r;
+  for (int i = 0; i < 14; i++) r.d[i] = dpp_q(a.x.d[i]);
+  return {r};
 }
-__device__ __forceinline__ Fp h_fp(const Fp& a) {
-  Fp r;
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ FqB<V, D> dh(const FqB<V, D>& a) {
+  Fq r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.l[i] = dpp_h(a.l[i]);
-  return r;
+  for (int i = 0; i < 14; i++) r.d[i] = dpp_h(a.x.d[i]);
+  return {r};
 }
-__device__ __forceinline__ Fp2 q_fp2(const Fp2& a) { return Fp2{q_fp(a.c0), q_fp(a.c1)}; }
-__device__ __forceinline__ Fp2 h_fp2(const Fp2& a) { return Fp2{h_fp(a.c0), h_fp(a.c1)}; }
-__device__ __forceinline__ Fp6 h_fp6(const Fp6& a) { return Fp6{h_fp2(a.c0), h_fp2(a.c1), h_fp2(a.c2)}; }
-
-// X * Y in Fp6, three of its six Fp2 products on each q lane
-__device__ __forceinline__ Fp6 q6mul(const Fp6& X, const Fp6& Y, bool q) {
-  const Fp2 p0 = f2mul(sel_fp2(q, f2add_raw(X.c1, X.c2), X.c0), sel_fp2(q, f2add_raw(Y.c1, Y.c2), Y.c0));
-  SEQ();
-  const Fp2 p1 = f2mul(sel_fp2(q, f2add_raw(X.c0, X.c1), X.c1), sel_fp2(q, f2add_raw(Y.c0, Y.c1), Y.c1));
-  SEQ();
-  const Fp2 p2 = f2mul(sel_fp2(q, f2add_raw(X.c0, X.c2), X.c2), sel_fp2(q, f2add_raw(Y.c0, Y.c2), Y.c2));
-  SEQ();
-  const Fp2 o0 = q_fp2(p0), o1 = q_fp2(p1), o2 = q_fp2(p2);
-  const Fp2 t0 = sel_fp2(q, o0, p0), t1 = sel_fp2(q, o1, p1), t2 = sel_fp2(q, o2, p2);
-  const Fp2 u0 = sel_fp2(q, p0, o0), u1 = sel_fp2(q, p1, o1), u2 = sel_fp2(q, p2, o2);
-  const Fp2 c0 = f2add(f2xi(f2sub(f2sub(u0, t1), t2)), t0);
-  const Fp2 c1 = f2add(f2sub(f2sub(u1, t0), t1), f2xi(t2));
-  const Fp2 c2 = f2add(f2sub(f2sub(u2, t0), t2), t1);
-  return Fp6{c0, c1, c2};
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq2B<V, D> dq2(const Fq2B<V, D>& a) {
+  return {dq(a.c0), dq(a.c1)};
+}
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq2B<V, D> dh2(const Fq2B<V, D>& a) {
+  return {dh(a.c0), dh(a.c1)};
+}
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq6B<V, D> dh6(const Fq6B<V, D>& a) {
+  return {dh2(a.c0), dh2(a.c1), dh2(a.c2)};
 }
 
-// one Fp12 squaring (a + b w)^2 = (a^2 + v b^2) + 2ab w: h = 0 forms u = (a + b)(a + v b), h = 1 forms
-// t = a b; then a' = u - t - v t, b' = 2 t
-__device__ __forceinline__ Fp6 q_sqr(const Fp6& own, bool h, bool q) {
-  const Fp6 oth = h_fp6(own);
-  const Fp6 A = sel_fp6(h, oth, own), Bv = sel_fp6(h, own, oth);
-  const Fp6 X = sel_fp6(h, A, f6add_raw(A, Bv));
-  const Fp6 Y = sel_fp6(h, Bv, f6add_raw(A, f6v(Bv)));
-  const Fp6 P = q6mul(X, Y, q);
-  const Fp6 t = h_fp6(P);
-  return sel_fp6(h, f6add(P, P), f6sub(f6sub(P, t), f6v(t)));
+// X * Y in Fp6, three of its six Fp2 products on each q lane (as q6mul)
+template <uint64_t VX, uint64_t DX, uint64_t VY, uint64_t DY>
+__device__ __forceinline__ auto qq6mul(const Fq6B<VX, DX>& X, const Fq6B<VY, DY>& Y, bool q) {
+  const auto p0 = sel(q, norm(X.c1 + X.c2), X.c0) * sel(q, norm(Y.c1 + Y.c2), Y.c0);
+  SEQ();
+  const auto p1 = sel(q, norm(X.c0 + X.c1), X.c1) * sel(q, norm(Y.c0 + Y.c1), Y.c1);
+  SEQ();
+  const auto p2 = sel(q, norm(X.c0 + X.c2), X.c2) * sel(q, norm(Y.c0 + Y.c2), Y.c2);
+  SEQ();
+  const auto o0 = dq2(p0), o1 = dq2(p1), o2 = dq2(p2);
+  const auto t0 = sel(q, o0, p0), t1 = sel(q, o1, p1), t2 = sel(q, o2, p2);
+  const auto u0 = sel(q, p0, o0), u1 = sel(q, p1, o1), u2 = sel(q, p2, o2);
+  const auto c0 = norm(xi(norm(u0 - (t1 + t2))) + t0);
+  const auto c1 = norm((u1 - (t0 + t1)) + xi(t2));
+  const auto c2 = norm((u2 - (t0 + t2)) + t1);
+  return fq6b(c0, c1, c2);
 }
 
-// own *= line: h = 0: a' = a (l0, l2) + v (b l3 v);  h = 1: b' = b (l0, l2) + a (l3 v)
-__device__ __forceinline__ Fp6 q_line(const Fp6& own, bool h, bool q, const Fp2& l0, const Fp2& l2, const Fp2& l3) {
-  const Fp6 oth = h_fp6(own);
-  const Fp2 p1 = f2mul(sel_fp2(q, f2add_raw(own.c0, own.c1), own.c0), sel_fp2(q, f2add_raw(l0, l2), l0));
-  SEQ();
-  const Fp2 p2 = f2mul(sel_fp2(q, oth.c2, own.c1), sel_fp2(q, l3, l2));
-  SEQ();
-  const Fp2 p3 = f2mul(sel_fp2(q, oth.c0, own.c2), sel_fp2(q, l3, l2));
-  SEQ();
-  const Fp2 p4 = f2mul(sel_fp2(q, oth.c1, own.c2), sel_fp2(q, l3, l0));
-  SEQ();
-  const Fp2 o1 = q_fp2(p1), o2 = q_fp2(p2), o3 = q_fp2(p3), o4 = q_fp2(p4);
-  // q = 0 products: t0 = a_0 l0, t1 = a_1 l2, u0 = a_2 l2, u2 = a_2 l0
-  const Fp2 t0 = sel_fp2(q, o1, p1), t1 = sel_fp2(q, o2, p2), u0 = sel_fp2(q, o3, p3), u2 = sel_fp2(q, o4, p4);
-  // q = 1 products: u1 = (a_0 + a_1)(l0 + l2), v_k = o_{k-1} l3
-  const Fp2 u1 = sel_fp2(q, p1, o1), v0 = sel_fp2(q, p2, o2), v1 = sel_fp2(q, p3, o3), v2 = sel_fp2(q, p4, o4);
-  const Fp6 m01{f2add(t0, f2xi(u0)), f2sub(f2sub(u1, t0), t1), f2add(t1, u2)};
-  const Fp6 m1{f2xi(v0), v1, v2};
-  return f6add(m01, sel_fp6(h, m1, f6v(m1)));
+// one Fp12 squaring on the (h, q) lanes, as q_sqr
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ auto qq_sqr(const Fq6B<V, D>& own, bool h, bool q) {
+  const auto oth = dh6(own);
+  const auto A = sel(h, oth, own), Bv = sel(h, own, oth);
+  const auto X = norm(sel(h, A, A + Bv));
+  const auto Y = norm(sel(h, Bv, A + f6v(Bv)));
+  const auto P = qq6mul(X, Y, q);
+  const auto t = dh6(P);
+  return norm(sel(h, P + P, (P - t) - f6v(t)));
 }
 
-// line record of pair p at its step pointer Li: (l0, E*ZZ or r, z3*ZZ or z3); lane (h, q) forms
-// component q of (h ? z3*ZZ * y_P : E*ZZ * (-x_P)), then two exchanges give l2, l3 on every lane
-__device__ __forceinline__ void q_line_p(const uint32_t* Li, size_t n, bool h, bool q, const Fp& nxP, const Fp& yP,
-                                         Fp2& l2, Fp2& l3) {
+// own *= line, as q_line
+template <uint64_t V, uint64_t D, uint64_t VL, uint64_t DL, uint64_t VM, uint64_t DM>
+__device__ __forceinline__ auto qq_line(const Fq6B<V, D>& own, bool h, bool q, const Fq2B<VL, DL>& l0,
+                                        const Fq2B<VM, DM>& l2, const Fq2B<VM, DM>& l3) {
+  // the other half's coefficients are exchanged one at a time, right before their product (live range)
+  const auto p1 = sel(q, norm(own.c0 + own.c1), own.c0) * sel(q, norm(l0 + l2), l0);
+  SEQ();
+  const auto p2 = sel(q, dh2(own.c2), own.c1) * sel(q, l3, l2);
+  SEQ();
+  const auto p3 = sel(q, dh2(own.c0), own.c2) * sel(q, l3, l2);
+  SEQ();
+  const auto p4 = sel(q, dh2(own.c1), own.c2) * sel(q, l3, l0);
+  SEQ();
+  const auto o1 = dq2(p1), o2 = dq2(p2), o3 = dq2(p3), o4 = dq2(p4);
+  const auto t0 = sel(q, o1, p1), t1 = sel(q, o2, p2), u0 = sel(q, o3, p3), u2 = sel(q, o4, p4);
+  const auto u1 = sel(q, p1, o1), v0 = sel(q, p2, o2), v1 = sel(q, p3, o3), v2 = sel(q, p4, o4);
+  const auto m01 = fq6b(t0 + xi(u0), (u1 - (t0 + t1)), t1 + u2);
+  const auto m1 = fq6b(xi(v0), v1, v2);
+  return norm(norm(m01) + norm(sel(h, m1, f6v(m1))));
+}
+
+// one line's inputs on lane (h, q): l0 and the coefficient this lane scales (component q of E ZZ for h = 0, of
+// z3 ZZ for h = 1).  (Loading them one line ahead of use measured 3.72 ms per launch against 3.68 ms without, and
+// the 512-register allocation it needed cost ~15 % of pipelined throughput.)
+struct LineIn {
+  Fp2 l0;
   Fp c;
+};
+__device__ __forceinline__ LineIn ld_line(const uint32_t* Li, size_t n, bool h, bool q) {
+  LineIn r;
+  r.l0 = ml_load2(Li, n, 0);
   const int w0 = (h ? 48 : 24) + (q ? 12 : 0);
 #pragma unroll
-  for (int j = 0; j < 12; ++j) c.l[j] = Li[(size_t)(w0 + j) * n];
-  const Fp mine = fp_mul_i(c, h ? yP : nxP);
-  const Fp part = q_fp(mine);
-  const Fp2 m{sel_fp(q, part, mine), sel_fp(q, mine, part)};
-  const Fp2 o = h_fp2(m);
-  l2 = sel_fp2(h, o, m);
-  l3 = sel_fp2(h, m, o);
+  for (int j = 0; j < 12; ++j) r.c.l[j] = Li[(size_t)(w0 + j) * n];
+  return r;
+}
+
+// the line's P factors, as q_line_p: l2 = E ZZ (-x_P), l3 = z3 ZZ y_P in N form
+__device__ __forceinline__ void qq_line_p(const LineIn& in, const G1A* PP, bool h, bool q, Fq2B<2, fqb_detail::MASK>& l2,
+                                          Fq2B<2, fqb_detail::MASK>& l3) {
+  const FqC pc = fqb_canon(h ? PP->y : PP->x);
+  const FqN mine = fqb_canon(in.c) * sel(h, pc, FqC{fq_zero()} - pc);  // -x_P as K - x_P (K a multiple of p)
+  const FqN part = dq(mine);
+  const Fq2B<2, fqb_detail::MASK> m{sel(q, part, mine), sel(q, mine, part)};
+  const auto o = dh2(m);
+  l2 = sel(h, o, m);
+  l3 = sel(h, m, o);
 }
 
 }  // namespace
 
 template <int G>
-__global__ void __launch_bounds__(64) k_miller_acc4(const G1A* P, const G2A* Q, const int* ok, size_t n,
-                                                    const uint32_t* L, Fp12* out) {
+__global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q, const int* ok, size_t n,
+                                                     const uint32_t* L, Fp12* out) {
   const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
   const size_t grp = t >> 2;
   const bool h = (t & 2) != 0, q = (t & 1) != 0;
@@ -176,35 +199,38 @@ __global__ void __launch_bounds__(64) k_miller_acc4(const G1A* P, const G2A* Q, 
     }
     return;
   }
+  constexpr uint64_t VF = ML_QF_V, DF = ML_QF_D;
+  using F = Fq6B<VF, DF>;
   const size_t step = (size_t)ML_WORDS2 * n;
-  const uint32_t* Li[G];
+  const uint32_t* Lb[G];
 #pragma unroll
-  for (int g = 0; g < G; ++g) Li[g] = L + pi[g];
-  Fp6 f{h ? fp2_zero() : fp2_one(), fp2_zero(), fp2_zero()};
+  for (int g = 0; g < G; ++g) Lb[g] = L + pi[g];
+  const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
+  const Fq2B<1, fqb_detail::MASK> z2{zero, zero};
+  F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = q_sqr(f, h, q);
+    if (b != 62) f = relax<VF, DF>(qq_sqr(f, h, q));
     const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
 #pragma unroll 1
     for (int s = 0; s < nl; ++s) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        // P coordinates re-read per step (cached; keeps them out of the live registers)
-        const G1A* pp = P + pi[g];
-        const Fp nxP = fp_neg(pp->x), yP = pp->y;
-        Fp2 l2, l3;
-        q_line_p(Li[g], n, h, q, nxP, yP, l2, l3);
-        const Fp6 fl = q_line(f, h, q, ml_load2(Li[g], n, 0), l2, l3);
-        f = G == 1 ? fl : sel_fp6(live[g], fl, f);
-        Li[g] += step;
+        const LineIn cur = ld_line(Lb[g], n, h, q);
+        Fq2B<2, fqb_detail::MASK> l2, l3;
+        qq_line_p(cur, P + pi[g], h, q, l2, l3);
+        const auto fl = relax<VF, DF>(qq_line(f, h, q, fq2b_canon(cur.l0), l2, l3));
+        f = G == 1 ? fl : sel(live[g], fl, f);
+        Lb[g] += step;
       }
     }
   }
   if (!q) {
+    Fp6 r{fq2b_pack(f.c0), fq2b_pack(f.c1), fq2b_pack(f.c2)};
     if (h)
-      out[grp].c1 = Fp6{fp2_neg(f.c0), fp2_neg(f.c1), fp2_neg(f.c2)};
+      out[grp].c1 = Fp6{fp2_neg(r.c0), fp2_neg(r.c1), fp2_neg(r.c2)};
     else
-      out[grp].c0 = f;
+      out[grp].c0 = r;
   }
 }
 
@@ -214,9 +240,9 @@ hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const 
   const size_t ngrp = (n + G - 1) / G;
   const dim3 grid((unsigned)((4 * ngrp + 63) / 64));
   if (G == 2)
-    hipLaunchKernelGGL(k_miller_acc4<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
+    hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
   else
-    hipLaunchKernelGGL(k_miller_acc4<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
+    hipLaunchKernelGGL(k_miller_acc4q<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
   return hipGetLastError();
 }
 

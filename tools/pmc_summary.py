@@ -22,16 +22,20 @@ def main(path, out=None):
         dur[k][row["Dispatch_Id"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
     lds_pass = any("SQ_LDS_IDX_ACTIVE" in acc[k] for k in acc)
     fetch_pass = any("FETCH_SIZE" in acc[k] for k in acc)
-    if fetch_pass:  # FETCH_SIZE is in KB (MI355X_MICROARCH.md, rocprofv3 section); uncorrected
-        lines = [f"# rocprofv3 --pmc FETCH_SIZE summary of {path} (per dispatch averages, uncorrected)",
-                 "| kernel | disp | ms | FETCH_SIZE KB/dispatch | MB/dispatch | GB/s |",
-                 "|---|---|---|---|---|---|"]
+    if fetch_pass:  # FETCH_SIZE is in KB (MI355X_MICROARCH.md, rocprofv3 section)
+        # gfx950: FETCH_SIZE = TCC_EA0_RDREQ x 64 B while the requests are 128 B, so a 16-B-per-lane read (every
+        # bulk load of these kernels: registry records, line records) reports half its bytes -- doubled here
+        lines = [f"# rocprofv3 --pmc FETCH_SIZE summary of {path} (per dispatch averages; 'corrected' = x2, the "
+                 "gfx950 correction for 16-B/lane reads, MI355X_MICROARCH.md HBM section)",
+                 "| kernel | disp | ms | FETCH_SIZE KB/dispatch (raw) | MB/dispatch (raw) | MB/dispatch (corrected) | "
+                 "GB/s (corrected) |",
+                 "|---|---|---|---|---|---|---|"]
         for k in sorted(acc, key=lambda k: -sum(dur[k].values())):
             n = len(disp[k])
             kb = acc[k].get("FETCH_SIZE", 0) / n
             ms = sum(dur[k].values()) / n
-            lines.append(f"| {k} | {n} | {ms:.3f} | {kb:.0f} | {kb * 1024 / 1e6:.2f} | "
-                         f"{kb * 1024 / (ms * 1e-3) / 1e9 if ms else 0:.1f} |")
+            lines.append(f"| {k} | {n} | {ms:.3f} | {kb:.0f} | {kb * 1024 / 1e6:.2f} | {2 * kb * 1024 / 1e6:.2f} | "
+                         f"{2 * kb * 1024 / (ms * 1e-3) / 1e9 if ms else 0:.1f} |")
         text = "\n".join(lines) + "\n"
         if out:
             open(out, "w").write(text)
