@@ -12,6 +12,7 @@
 #include "bls_fq_g2.h"
 #include "bls_pp_lane.h"
 #include "bls_vm.h"
+#include "bls_xmd32.h"
 
 namespace bls {
 
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(64) k_g1_affine_b(size_t B, const int* status,
     acc = fp_mul_i(acc, zero[k] ? FP_ONE : z);
     pre[k] = acc;
   }
-  Fp inv = fp_inv(acc);  // 1 / (z_0 ... z_{K-1})
+  Fp inv = fp_inv_i(acc);  // 1 / (z_0 ... z_{K-1})
 #pragma unroll
   for (int k = AFF_K - 1; k >= 0; --k) {
     const size_t i = base + 64 * k;
@@ -138,7 +139,7 @@ __global__ void __launch_bounds__(64) k_h2c_affine_b(size_t B, const int* status
     acc = fp_mul_i(acc, zero[k] ? FP_ONE : n);
     pre[k] = acc;
   }
-  Fp inv = fp_inv(acc);
+  Fp inv = fp_inv_i(acc);
 #pragma unroll
   for (int k = AFF_K - 1; k >= 0; --k) {
     const size_t i = base + 64 * k;
@@ -169,26 +170,35 @@ __device__ __forceinline__ PP<Fp2> pp2_sel(bool c, const PP<Fp2>& a, const PP<Fp
 }
 
 // (x, y) affine on E2' -> iso(x, y) = (xnum yden : y ynum xden : xden yden) on E2 (RFC 9380 App. E.3)
+// (the products run one after another: interleaved, their digit columns pushed the kernel into spills)
+#define H2C_SEQ() __builtin_amdgcn_sched_barrier(0)
 __device__ __forceinline__ PP<Fp2> iso_proj_lane(const Fp2& x, const Fp2& y) {
-  const Fp2 xx = f2sqr(x), xxx = f2mul(xx, x);
+  const Fp2 xx = f2sqr(x);
+  H2C_SEQ();
+  const Fp2 xxx = f2mul(xx, x);
+  H2C_SEQ();
   const Fp2 xnum = fadd(fadd(f2mul(ISO_XNUM_3, xxx), f2mul(ISO_XNUM_2, xx)), fadd(f2mul(ISO_XNUM_1, x), ISO_XNUM_0));
+  H2C_SEQ();
   const Fp2 xden = fadd(fadd(xx, f2mul(ISO_XDEN_1, x)), ISO_XDEN_0);
+  H2C_SEQ();
   const Fp2 ynum = fadd(fadd(f2mul(ISO_YNUM_3, xxx), f2mul(ISO_YNUM_2, xx)), fadd(f2mul(ISO_YNUM_1, x), ISO_YNUM_0));
+  H2C_SEQ();
   const Fp2 yden = fadd(fadd(xxx, f2mul(ISO_YDEN_2, xx)), fadd(f2mul(ISO_YDEN_1, x), ISO_YDEN_0));
-  return PP<Fp2>{f2mul(xnum, yden), f2mul(f2mul(y, ynum), xden), f2mul(xden, yden)};
+  H2C_SEQ();
+  const Fp2 X = f2mul(xnum, yden);
+  H2C_SEQ();
+  const Fp2 Y = f2mul(f2mul(y, ynum), xden);
+  H2C_SEQ();
+  return PP<Fp2>{X, Y, f2mul(xden, yden)};
 }
 
-// lane 0 writes X, Y.c0; lane 1 Y.c1, Z (six consecutive Fd slots)
+// lane 0 writes X, Y.c0; lane 1 Y.c1, Z (six consecutive Fd slots).  Selects, not a branch on the lane: the
+// branch kept the point in a private-memory copy.
 __device__ __forceinline__ void pp2_store(Fd* o, const PP<Fp2>& p, bool hi) {
-  if (!hi) {
-    o[0] = fd_from_fp(p.x.c0);
-    o[1] = fd_from_fp(p.x.c1);
-    o[2] = fd_from_fp(p.y.c0);
-  } else {
-    o[3] = fd_from_fp(p.y.c1);
-    o[4] = fd_from_fp(p.z.c0);
-    o[5] = fd_from_fp(p.z.c1);
-  }
+  Fd* d = o + (hi ? 3 : 0);
+  d[0] = fd_from_fp(fp_select(hi, p.y.c1, p.x.c0));
+  d[1] = fd_from_fp(fp_select(hi, p.z.c0, p.x.c1));
+  d[2] = fd_from_fp(fp_select(hi, p.z.c1, p.y.c0));
 }
 __device__ __forceinline__ PP<Fp2> pp2_load(const Fd* in) {
   return PP<Fp2>{Fp2{fp_from_fd(in[0]), fp_from_fd(in[1])}, Fp2{fp_from_fd(in[2]), fp_from_fd(in[3])},
@@ -197,7 +207,10 @@ __device__ __forceinline__ PP<Fp2> pp2_load(const Fd* in) {
 
 }  // namespace
 
-// msgs: 32-byte messages (offs == nullptr) or msgs[offs[i] .. offs[i+1]); status: items to skip (may be null)
+// VAR = false: 32-byte messages msgs[32 i ..] (the FastAggregateVerify batches), hashed by the register-resident
+// expand_message_xmd of bls_xmd32.h; VAR = true: msgs[offs[i] .. offs[i+1]) of any length (the byte-streaming
+// bls_sha256.h).  status: items to skip (may be null)
+template <bool VAR>
 __global__ void __launch_bounds__(64) k_h2c_sswu_iso2(size_t B, const uint8_t* msgs, const uint64_t* offs,
                                                       const int* status, Fd* hf, int* flag) {
   const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
@@ -211,15 +224,20 @@ __global__ void __launch_bounds__(64) k_h2c_sswu_iso2(size_t B, const uint8_t* m
     return;
   }
   Fp2 u[2];
-  if (offs)
+  if (VAR)
     hash_to_field_fp2(u, msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_FAV, 43);
   else
-    hash_to_field_fp2(u, msgs + 32 * i, 32, DST_POP_FAV, 43);
+    hash_to_field_fp2_m32(u, msgs + 32 * i);
+  H2C_SEQ();
   Fp2 x, y;
-  map_to_curve_sswu_lane(x, y, hi ? u[1] : u[0]);
+  bool rare;
+  map_to_curve_sswu_lane_i(x, y, hi ? u[1] : u[0], rare);
+  H2C_SEQ();
   const PP<Fp2> mine = iso_proj_lane(x, y);
+  H2C_SEQ();
   const PP<Fp2> other = pp2_swap(mine);
-  const uint32_t bad = fp2_is_zero(mine.z) ? 1u : 0u;  // an isogeny denominator vanished: k_h2c_fallback
+  // an isogeny denominator vanished, or an SSWU case this kernel does not compute: k_h2c_fallback
+  const uint32_t bad = (rare || fp2_is_zero(mine.z)) ? 1u : 0u;
   const uint32_t any_bad = bad | cl_swap(bad);
   const PP<Fp2> Q = pp2_add(pp2_sel(hi, other, mine), pp2_sel(hi, mine, other), hi);
   pp2_store(o, Q, hi);
@@ -244,38 +262,56 @@ __device__ __forceinline__ void pp_store1(Fd* o, const PP<Fp2>& p) {
   o[5] = fd_from_fp(p.z.c1);
 }
 
-// [|x|] of a projective point through the digit-form Jacobian chain (bls_fq_g2.h): (X Z, Y Z^2, Z) in, (X Z, Y, Z^3)
-// out, canonical packed
-// (noinline: one copy for both kernels; a call per chain is nothing against its 68 steps, and inlined twice it
-// doubled this file's device compile time)
-__device__ __noinline__ PP<Fp2> pp_mul_xabs_q(const PP<Fp2>& P, bool& exc) {
+// [|x|] of a projective point through the digit-form Jacobian chain (bls_fq_g2.h, base point parked in LDS): (X Z,
+// Y Z^2, Z) in, (X Z, Y, Z^3) out, canonical packed.  Inline and call-free: the out-of-line chain cost each
+// kernel a 1.5-2 KB private segment.
+__device__ __forceinline__ PP<Fp2> pp_mul_xabs_q(const PP<Fp2>& P, bool& exc, uint32_t* lds) {
   const Fq2 z = fq2_unpack(P.z);
   const J2Q J{fq2_mul(fq2_unpack(P.x), z), fq2_mul(fq2_unpack(P.y), fq2_sqr(z)), z};
-  const J2Q M = j2q_mul_xabs(J, exc);
+  const J2Q M = j2q_mul_xabs_lds(J, exc, lds);
   return PP<Fp2>{fq2_pack(fq2_mul(M.x, M.z)), fq2_pack(M.y), fq2_pack(fq2_mul(fq2_sqr(M.z), M.z))};
 }
+// the staged inputs are re-read from HBM after the chain instead of being held across it (the barrier keeps the
+// compiler from reusing the first load)
+#define H2C_RELOAD_BARRIER() asm volatile("" ::: "memory")
+
 __global__ void __launch_bounds__(64) k_g2x_pre1t(size_t B, const int* status, Fd* hf, int* flag) {
+  __shared__ uint32_t lds[84 * 64];
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B || (status && !status[i])) return;
   Fd* r = hf + HCF * i;
-  const PP<Fp2> Q = pp2_load(r + HCF_Q);
   bool exc = false;
-  const PP<Fp2> M = pp_mul_xabs_q(Q, exc);
-  const PP<Fp2> pq = pp_psi2x(Q);
-  pp_store1(r + HCF_A, pp_add(pq, pp_neg2(M)));  // t1 + t2, t1 = -M
-  const PP<Fp2> mq = pp_add(M, pp_neg2(Q));
-  const PP<Fp2> t3{f2mul(Q.x, PSI2_CX), f2mul(Q.y, PSI2_CY), Q.z};  // psi^2(Q); psi^2(2Q) = 2 psi^2(Q)
-  pp_store1(r + HCF_C, pp_add(pp_add(pp_dbl(t3), pp_neg2(pq)), mq));
+  pp_store1(r + HCF_M, pp_mul_xabs_q(pp2_load(r + HCF_Q), exc, lds));  // M = [|x|] Q
+  // the complete-formula steps, each from points re-read from the staging slots so at most ~3 points are live
+  // (held across all of them, five points spilled ~450 VGPRs)
+  H2C_RELOAD_BARRIER();
+  {
+    const PP<Fp2> pq = pp_psi2x(pp2_load(r + HCF_Q));
+    pp_store1(r + HCF_A, pp_add(pq, pp_neg2(pp2_load(r + HCF_M))));  // A = psi(Q) - M  (t1 + t2, t1 = -M)
+  }
+  H2C_RELOAD_BARRIER();
+  {
+    const PP<Fp2> Q = pp2_load(r + HCF_Q);
+    const PP<Fp2> pq = pp_psi2x(Q);
+    const PP<Fp2> t3{f2mul(Q.x, PSI2_CX), f2mul(Q.y, PSI2_CY), Q.z};  // psi^2(Q); psi^2(2Q) = 2 psi^2(Q)
+    pp_store1(r + HCF_C, pp_add(pp_dbl(t3), pp_neg2(pq)));          // psi^2(2Q) - psi(Q)
+  }
+  H2C_RELOAD_BARRIER();
+  {
+    const PP<Fp2> mq = pp_add(pp2_load(r + HCF_M), pp_neg2(pp2_load(r + HCF_Q)));  // M - Q
+    pp_store1(r + HCF_C, pp_add(pp2_load(r + HCF_C), mq));
+  }
   if (exc) flag[i] = 1;
 }
 
 __global__ void __launch_bounds__(64) k_g2x_post1t(size_t B, const int* status, Fd* hf, int* flag) {
+  __shared__ uint32_t lds[84 * 64];
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B || (status && !status[i])) return;
   Fd* r = hf + HCF * i;
   bool exc = false;
-  const PP<Fp2> A = pp2_load(r + HCF_A);
-  const PP<Fp2> M = pp_mul_xabs_q(A, exc);
+  const PP<Fp2> M = pp_mul_xabs_q(pp2_load(r + HCF_A), exc, lds);
+  H2C_RELOAD_BARRIER();
   pp_store1(r + HCF_A, pp_add(pp2_load(r + HCF_C), pp_neg2(M)));  // projective H over the dead A slots
   if (exc) flag[i] = 1;
 }
@@ -288,7 +324,10 @@ size_t h2c_scratch_fd(size_t B) { return (size_t)HCF * B; }
 // msgs: 32-byte messages (offs == nullptr) or msgs[offs[i] .. offs[i+1]); status: items to skip (may be null)
 static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs,
                                    const int* status, Fd* hf, G2A* H, int* flag) {
-  hipLaunchKernelGGL(k_h2c_sswu_iso2, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, status, hf, flag);
+  if (offs)
+    hipLaunchKernelGGL(k_h2c_sswu_iso2<true>, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, status, hf, flag);
+  else
+    hipLaunchKernelGGL(k_h2c_sswu_iso2<false>, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, status, hf, flag);
   hipLaunchKernelGGL(k_g2x_pre1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
   hipLaunchKernelGGL(k_g2x_post1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
   hipLaunchKernelGGL(k_h2c_affine_b, dim3(nblk(B, 64 * AFF_K)), dim3(64), 0, st, B, status, hf, H);

@@ -300,6 +300,33 @@ BLS_HDNI Fp fp_inv(const Fp& a) {
   return fp_mul(r, FP_R3);
 }
 
+// fp_inv inline (the lane kernels on per-job streams: an out-of-line call costs the kernel a private segment)
+BLS_HD Fp fp_inv_i(const Fp& a) {
+  if (fp_is_zero(a)) return a;
+  Fp u = a, v, x1 = fp_zero(), x2 = fp_zero();
+#pragma unroll
+  for (int i = 0; i < 12; i++) v.l[i] = P_LIMBS[i];
+  x1.l[0] = 1;
+  while (!raw_is_one(u) && !raw_is_one(v)) {
+    while (raw_is_even(u)) {
+      raw_shr1(u, 0);
+      half_mod_p(x1);
+    }
+    while (raw_is_even(v)) {
+      raw_shr1(v, 0);
+      half_mod_p(x2);
+    }
+    if (raw_geq(u, v)) {
+      raw_sub(u, v);
+      x1 = fp_sub(x1, x2);
+    } else {
+      raw_sub(v, u);
+      x2 = fp_sub(x2, x1);
+    }
+  }
+  return fp_mul_i(raw_is_one(u) ? x1 : x2, FP_R3);
+}
+
 BLS_HDNI Fp fp_inv_fermat(const Fp& a) { return fp_pow(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
 
 BLS_HD bool fp_is_one(const Fp& a) { return fp_eq(a, FP_ONE); }

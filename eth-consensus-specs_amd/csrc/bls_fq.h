@@ -262,7 +262,9 @@ BLS_HD Fq fq_pow_w3(const Fq& a, const uint32_t* e, int nbits) {
     while (!((e[j >> 5] >> (j & 31)) & 1u)) ++j;
     uint32_t w = 0;
     for (int k = i; k >= j; --k) w = (w << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
-    const Fq& m = w == 1u ? t1 : (w == 3u ? t3 : (w == 5u ? t5 : t7));
+    // a value select, not a reference to one of the four: a reference chosen at run time made them addressable
+    // (a private-memory copy of t1..t7 in every kernel that inlines this)
+    const Fq m = fq_select(w == 1u, t1, fq_select(w == 3u, t3, fq_select(w == 5u, t5, t7)));
     if (!started) {
       r = m;
       started = true;

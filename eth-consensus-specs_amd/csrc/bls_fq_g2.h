@@ -15,6 +15,15 @@
 
 namespace bls {
 
+// Order the Fq2 products of a chain step one after another on the device: the scheduler interleaved the
+// independent products of a doubling / addition and held so many digit columns live that an inlined chain
+// spilled ~300 VGPRs (the host build has nothing to order).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FQ_SEQ() __builtin_amdgcn_sched_barrier(0)
+#else
+#define FQ_SEQ() ((void)0)
+#endif
+
 template <const uint32_t* K>
 BLS_HD Fq fq_subk(const Fq& a, const Fq& b) {
   FQ_CHECK_SUB(b, K);
@@ -53,36 +62,84 @@ struct J2Q {
 // dbl-2009-l: X < 1030p, Y < 650p, Z < 270p in -> X3 < 1028p, Y3 < 194p, Z3 < 260p
 BLS_HD J2Q j2q_dbl(const J2Q& p) {
   const Fq2 A = fq2_sqr(p.x);                                      // (2, 4)
+  FQ_SEQ();
   const Fq2 Bq = fq2_sqr(p.y);
+  FQ_SEQ();
   const Fq2 C = fq2_sqr(Bq);
+  FQ_SEQ();
   const Fq2 XB2 = fq2_sqr(fq2_norm(fq2_add(p.x, Bq)));
+  FQ_SEQ();
   const Fq2 D = fq2_mul_small(fq2_subk<Q29_K2>(XB2, fq2_add(A, C)), 2);  // 2 (XB2 - A - C + 128p) < 264p
   const Fq2 E = fq2_mul_small(A, 3);                               // < 12p
   J2Q r;
   r.x = fq2_norm(fq2_subk<Q29_K1024>(fq2_sqr(E), fq2_mul_small(D, 2)));  // F - 2D + 1024p < 1028p
+  FQ_SEQ();
   const Fq2 DX = fq2_norm(fq2_subk<Q29_K2048_2>(D, r.x));         // < 2312p
   r.y = fq2_norm(fq2_subk<Q29_K1>(fq2_mul(E, DX), fq2_mul_small(C, 8)));  // < 194p
+  FQ_SEQ();
   r.z = fq2_mul_small(fq2_mul(p.y, p.z), 2);                       // < 260p
+  FQ_SEQ();
   return r;
 }
 
 // add-2007-bl (incomplete): exc |= the exceptional cases (h = 0, an identity operand), checked on canonical values
 BLS_HD J2Q j2q_add(const J2Q& p, const J2Q& q, bool& exc) {
-  const Fq2 z1z1 = fq2_sqr(p.z), z2z2 = fq2_sqr(q.z);
-  const Fq2 u1 = fq2_mul(p.x, z2z2), u2 = fq2_mul(q.x, z1z1);        // (66, 130)
-  const Fq2 s1 = fq2_mul(fq2_mul(p.y, q.z), z2z2), s2 = fq2_mul(fq2_mul(q.y, p.z), z1z1);
+  const Fq2 z1z1 = fq2_sqr(p.z);
+  FQ_SEQ();
+  const Fq2 z2z2 = fq2_sqr(q.z);
+  FQ_SEQ();
+  const Fq2 u1 = fq2_mul(p.x, z2z2);
+  FQ_SEQ();
+  const Fq2 u2 = fq2_mul(q.x, z1z1);        // (66, 130)
+  FQ_SEQ();
+  const Fq2 s1 = fq2_mul(fq2_mul(p.y, q.z), z2z2);
+  FQ_SEQ();
+  const Fq2 s2 = fq2_mul(fq2_mul(q.y, p.z), z1z1);
+  FQ_SEQ();
   const Fq2 h = fq2_norm(fq2_subk<Q29_K256>(u2, u1));              // < 386p
   exc = exc || fp2_is_zero(fq2_pack(h)) || fp2_is_zero(fq2_pack(p.z)) || fp2_is_zero(fq2_pack(q.z));
+  FQ_SEQ();
   const Fq2 rr = fq2_mul_small(fq2_subk<Q29_K256>(s2, s1), 2);     // < 772p
   const Fq2 i = fq2_sqr(fq2_mul_small(h, 2));
-  const Fq2 j = fq2_mul(h, i), v = fq2_mul(u1, i);
+  FQ_SEQ();
+  const Fq2 j = fq2_mul(h, i);
+  FQ_SEQ();
+  const Fq2 v = fq2_mul(u1, i);
+  FQ_SEQ();
   J2Q r;
   r.x = fq2_norm(fq2_subk<Q29_K512_2>(fq2_sqr(rr), fq2_add(j, fq2_mul_small(v, 2))));  // < 516p
+  FQ_SEQ();
   const Fq2 vx = fq2_norm(fq2_subk<Q29_K1024>(v, r.x));           // < 1154p
   r.y = fq2_norm(fq2_subk<Q29_K512_2>(fq2_mul(rr, vx), fq2_mul_small(fq2_mul(s1, j), 2)));  // < 642p
+  FQ_SEQ();
   const Fq2 zz = fq2_norm(fq2_subk<Q29_K2>(fq2_sqr(fq2_norm(fq2_add(p.z, q.z))), fq2_add(z1z1, z2z2)));
+  FQ_SEQ();
   r.z = fq2_mul(zz, h);                                              // (66, 130)
+  FQ_SEQ();
   return r;
+}
+
+// [|x|] p with the base point parked in LDS during the chain (lds: 84 words x 64 lanes, [word][lane]): it is read
+// only by the 5 additions, and the 84 registers it held pushed an inlined chain past the register file (~300
+// spilled VGPRs) -- in registers the chain had to be a separate call with a ~1.8 KB private segment.
+__device__ __forceinline__ J2Q j2q_mul_xabs_lds(const J2Q& p, bool& exc, uint32_t* lds) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(&p);
+#pragma unroll
+  for (int w = 0; w < 84; w++) lds[w * 64 + lane] = pw[w];
+  J2Q m = p;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    m = j2q_dbl(m);
+    if ((X_ABS >> b) & 1ull) {
+      J2Q q;
+      uint32_t* qw = reinterpret_cast<uint32_t*>(&q);
+#pragma unroll
+      for (int w = 0; w < 84; w++) qw[w] = lds[w * 64 + lane];
+      m = j2q_add(m, q, exc);
+    }
+  }
+  return m;
 }
 
 // [|x|] p (the leading bit of |x| is bit 63)

@@ -14,6 +14,7 @@
 #include "bls_curve.h"
 #include "bls_fq.h"
 #include "bls_sha256.h"
+#include "bls_tower_inline.h"
 
 namespace bls {
 
@@ -65,7 +66,9 @@ BLS_HDNI bool fp2_sqrt_lane(Fp2& out, const Fp2& a) {
 }
 
 BLS_HD int fp2_sgn0_lane(const Fp2& a_mont) {
-  const Fp a0 = fp_from_mont(a_mont.c0), a1 = fp_from_mont(a_mont.c1);
+  Fp one = fp_zero();
+  one.l[0] = 1;
+  const Fp a0 = fp_mul_i(a_mont.c0, one), a1 = fp_mul_i(a_mont.c1, one);  // out of Montgomery form, inline
   return (int)(a0.l[0] & 1u) | ((int)fp_is_zero(a0) & (int)(a1.l[0] & 1u));
 }
 
@@ -83,6 +86,46 @@ BLS_HD int fp2_sgn0_lane(const Fp2& a_mont) {
 // If g(x2) is used, g(x2) = Z^3 u^6 g(x1) and its norm root is K c norm(u)^3
 // with K = sqrt(-norm(Z)^3) (SSWU_K_NORM).  Ag = 0 (g(x1) = 0) keeps 1/D by a
 // Fermat inversion (unreachable for hash outputs in practice).
+// Inline form for the hash_to_G2 lane kernel: inline products (f2mul / f2sqr of bls_tower_inline.h; each
+// out-of-line fp2_mul / fp2_sqr call cost the kernel a call frame of private memory), everything used after an
+// exponentiation folded before it, so few values live across the exponentiation loops (zu2, xn conj(xd), ag d^4,
+// ag d, K norm(u)^3 and sgn0(u)), and no call: the two cases that need another exponentiation -- g(x1) = 0 and
+// g(x) in Fp -- are returned as `rare` (the caller's item goes to its reference-path fallback; neither occurs for
+// hash outputs in practice).  Otherwise the same x, y as map_to_curve_sswu_lane.
+BLS_HD void map_to_curve_sswu_lane_i(Fp2& x, Fp2& y, const Fp2& u, bool& rare) {
+  const int sgn_u = fp2_sgn0_lane(u);
+  const Fp2 zu2 = f2mul(SSWU_Z, f2sqr(u));
+  const Fp nu = fp_add(fp_sqr_i(u.c0), fp_sqr_i(u.c1));
+  const Fp knu3 = fp_mul_i(SSWU_K_NORM, fp_mul_i(fp_sqr_i(nu), nu));  // K norm(u)^3 (the g(x2) branch)
+  const Fp2 den = fp2_add(f2sqr(zu2), zu2);
+  const bool exc = fp2_is_zero(den);
+  const Fp2 xn = exc ? SSWU_B_OVER_ZA : f2mul(SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), den));
+  const Fp2 xd = exc ? fp2_one() : den;
+  const Fp2 xd2 = f2sqr(xd);
+  // gxn = xn^3 + A xn xd^2 + B xd^3
+  const Fp2 gxn = fp2_add(f2mul(fp2_add(f2sqr(xn), f2mul(SSWU_A, xd2)), xn), f2mul(SSWU_B, f2mul(xd2, xd)));
+  const Fp ag = fp_add(fp_sqr_i(gxn.c0), fp_sqr_i(gxn.c1));
+  const Fp d = fp_add(fp_sqr_i(xd.c0), fp_sqr_i(xd.c1));
+  const Fp d4 = fp_sqr_i(fp_sqr_i(d));
+  const Fp w = fp_mul_i(ag, fp_mul_i(d4, d));
+  const Fp2 xnc = f2mul(xn, fp2_conj(xd));
+  const Fp agd4 = fp_mul_i(ag, d4), agd = fp_mul_i(ag, d);
+  const bool ag0 = fp_is_zero(ag);
+  const Fp z = fp_pow_pm3_4(w);
+  const Fp z2 = fp_sqr_i(z);
+  const bool square = ag0 || fp_is_one(fp_mul_i(z2, w));  // chi(w) = 1 (or g(x1) = 0: y = 0)
+  Fp dinv = fp_mul_i(z2, agd4);  // chi / D
+  if (!square) dinv = fp_neg(dinv);
+  const Fp2 x1{fp_mul_i(xnc.c0, dinv), fp_mul_i(xnc.c1, dinv)};
+  const Fp c = fp_mul_i(agd, z);
+  x = square ? x1 : f2mul(zu2, x1);
+  const Fp2 gx = fp2_add(f2mul(fp2_add(f2sqr(x), SSWU_A), x), SSWU_B);
+  const Fp n = square ? c : fp_mul_i(knu3, c);
+  rare = ag0 || fp_is_zero(gx.c1);
+  Fp2 yy = fp2_sqrt_from_norm_root(gx, n);
+  if (sgn_u != fp2_sgn0_lane(yy)) yy = fp2_neg(yy);
+  y = yy;
+}
 BLS_HDNI void map_to_curve_sswu_lane(Fp2& x, Fp2& y, const Fp2& u) {
   const Fp2 u2 = fp2_sqr(u);
   const Fp2 zu2 = fp2_mul(SSWU_Z, u2);
@@ -127,6 +170,7 @@ BLS_HDNI void map_to_curve_sswu_lane(Fp2& x, Fp2& y, const Fp2& u) {
   if (fp2_sgn0_lane(u) != fp2_sgn0_lane(yy)) yy = fp2_neg(yy);
   y = yy;
 }
+
 
 // 96 bytes (x.c1 || x.c0) -> affine G2 (py_ecc signature_to_G2 rules); no
 // subgroup check.

@@ -2,17 +2,24 @@
 //
 // The 64-bit scalars split into 8 windows; the (item, window) pairs with a
 // nonzero digit d are counting-sorted into 8 x 255 buckets (atomic histogram,
-// one prefix pass, atomic scatter), and each bucket's points are added by a
-// lane pair (k_msm_bucket2, one mixed addition per step).  The bucket reduction is parallel:
-//   U_b = sum_{d : bit k of d} B_{w,d}   (b = 8w + k; 64 sums of 128 buckets,
-//                                          a 7-level pairwise tree), then
-//   S   = sum_b 2^b U_b                   (a 6-level tree of A + [2^k] B).
+// one block-wide prefix scan, atomic scatter).  Seven launches:
+//   k_msm_count, k_msm_scan, k_msm_scatter   the sort
+//   k_msm_bucketc   each bucket's points summed in MSM_C = 8 strided chunks,
+//                   one lane pair per chunk (~5 mixed additions each; 16,384
+//                   chunks = 512 waves, the point loads one step ahead)
+//   k_msm_usum      U_b = sum_{d : bit k of d} B_{w,d}  (b = 8w + k): one
+//                   workgroup per b, each lane pair sums its digit's 8 chunks,
+//                   then a 7-level tree through LDS
+//   k_msm_weighted  S = sum_b 2^b U_b: a 6-level tree through LDS pairing
+//                   node j with j + s and weighting it by 2^s (63 doublings on
+//                   the longest chain), then S -> affine
 // ~8 additions per signature instead of a 64-step double-and-add; the chain
 // runs on its own high-priority stream beside the Miller loops of the
-// (r_i apk_i, H_i) pairs.
+// (r_i apk_i, H_i) pairs.  (The previous form ran one lane pair per bucket --
+// 64 waves, ~40 dependent additions with unprefetched loads -- and 13 tree
+// launches: ~6.8 ms per C2 batch.)
 #include "bls_kernels.h"
 #include "bls_pp_lane.h"
-#include "bls_vm.h"
 
 #include <stdlib.h>
 
@@ -32,16 +39,33 @@ __global__ void __launch_bounds__(256) k_msm_count(size_t B, const int* status, 
   if (d) atomicAdd(&cnt[w * 256 + d], 1u);
 }
 
-// off[b] = exclusive prefix of cnt; cur[b] = off[b] (scatter cursor).
-__global__ void k_msm_scan(const uint32_t* cnt, uint32_t* off, uint32_t* cur) {
-  if (threadIdx.x || blockIdx.x) return;
-  uint32_t s = 0;
-  for (int b = 0; b < MSM_NB; b++) {
-    off[b] = s;
-    cur[b] = s;
-    s += cnt[b];
+// off[b] = exclusive prefix of cnt; cur[b] = off[b] (scatter cursor); one 256-thread block, 8 buckets per thread
+__global__ void __launch_bounds__(256) k_msm_scan(const uint32_t* cnt, uint32_t* off, uint32_t* cur) {
+  constexpr int PER = MSM_NB / 256;
+  __shared__ uint32_t part[256];
+  const int t = threadIdx.x;
+  uint32_t loc[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    loc[i] = cnt[t * PER + i];
+    sum += loc[i];
   }
-  off[MSM_NB] = s;
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan of the per-thread sums
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t base = part[t] - sum;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    off[t * PER + i] = base;
+    cur[t * PER + i] = base;
+    base += loc[i];
+  }
+  if (t == 255) off[MSM_NB] = part[255];
 }
 
 __global__ void __launch_bounds__(256) k_msm_scatter(size_t B, const int* status, const int* status2,
@@ -55,99 +79,114 @@ __global__ void __launch_bounds__(256) k_msm_scatter(size_t B, const int* status
   if (d) lst[atomicAdd(&cur[w * 256 + d], 1u)] = (uint32_t)i;
 }
 
-// U-tree input: ubase[(8w + k) * 128 + j] = B_{w, d_j} with d_j the j-th digit
-// having bit k set (bit k inserted into j).
-__global__ void __launch_bounds__(256) k_msm_gather_bits(const Fd* bsum, Fd* ubase) {
-  const int t = blockIdx.x * 256 + threadIdx.x;  // (b, j, coordinate)
-  if (t >= 64 * 128 * 6) return;
-  const int c = t % 6, j = (t / 6) % 128, b = t / (6 * 128);
-  const int w = b >> 3, k = b & 7;
-  const int d = ((j >> k) << (k + 1)) | (1 << k) | (j & ((1 << k) - 1));
-  ubase[t] = bsum[(size_t)(w * 256 + d) * 6 + c];
-}
+constexpr int MSM_C = 8;  // chunks per bucket
+using P2 = PP<Fp2>;
 
 // ----------------------------------------------------------- lane form --
-// The bucket sums and both reduction trees on lane pairs (bls_pp_lane.h pp2_*)
-// instead of wave programs: a bucket is ~40 sequential mixed additions, a tree
-// node one addition (after k doublings), so a 64-lane workgroup spent most of
-// its time staging slots and on per-level barriers for 4 items.  Same points
-// in the same projective form (complete formulas), same Fd staging.
+// Bucket, U and weighted sums on lane pairs (bls_pp_lane.h pp2_*: complete
+// projective formulas, each dependency level split between lanes 2k / 2k+1).
 namespace {
-__device__ __forceinline__ PP<Fp2> msm_load(const Fd* in) {
-  return PP<Fp2>{Fp2{fp_from_fd(in[0]), fp_from_fd(in[1])}, Fp2{fp_from_fd(in[2]), fp_from_fd(in[3])},
-                 Fp2{fp_from_fd(in[4]), fp_from_fd(in[5])}};
+// a point through LDS or HBM as six packed Fp: lane 0 of a pair writes x, y.c0, lane 1 y.c1, z
+__device__ __forceinline__ void p2_store(Fp* o, const P2& p, bool hi) {  // selects, not a branch: no stack copy
+  Fp* d = o + (hi ? 3 : 0);
+  d[0] = fp_select(hi, p.y.c1, p.x.c0);
+  d[1] = fp_select(hi, p.z.c0, p.x.c1);
+  d[2] = fp_select(hi, p.z.c1, p.y.c0);
 }
-__device__ __forceinline__ void msm_store(Fd* o, const PP<Fp2>& p, bool hi) {
-  if (!hi) {
-    o[0] = fd_from_fp(p.x.c0);
-    o[1] = fd_from_fp(p.x.c1);
-    o[2] = fd_from_fp(p.y.c0);
-  } else {
-    o[3] = fd_from_fp(p.y.c1);
-    o[4] = fd_from_fp(p.z.c0);
-    o[5] = fd_from_fp(p.z.c1);
-  }
+// 1 / (a0 + a1 i) = (a0 - a1 i) / (a0^2 + a1^2) with the inline Fp inverse (an out-of-line call here cost a
+// 960-B private segment on the job's stream)
+__device__ __forceinline__ Fp2 fp2_inv_inline(const Fp2& a) {
+  const Fp ni = fp_inv_i(fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1)));
+  return Fp2{fp_mul_i(a.c0, ni), fp_neg(fp_mul_i(a.c1, ni))};
+}
+__device__ __forceinline__ P2 p2_load(const Fp* in) {
+  return P2{Fp2{in[0], in[1]}, Fp2{in[2], in[3]}, Fp2{in[4], in[5]}};
 }
 }  // namespace
 
-// bucket b = (lane pair index): bsum[b] = sum of its points (identity (0 : 1 : 0) if empty)
-__global__ void __launch_bounds__(64) k_msm_bucket2(const uint32_t* off, const uint32_t* lst, const G2A* sig,
-                                                    Fd* bsum) {
+// chunk c of bucket b (lane pair (b, c)): csum[b C + c] = sum of the bucket's points k = off[b] + c + j C
+__global__ void __launch_bounds__(64) k_msm_bucketc(const uint32_t* off, const uint32_t* lst, const G2A* sig,
+                                                    Fp* csum) {
   const int t = blockIdx.x * 64 + threadIdx.x;
-  const int b = t >> 1;
+  const int pi = t >> 1;
   const bool hi = (t & 1) != 0;
-  if (b >= MSM_NB) return;
-  PP<Fp2> R{fp2_zero(), fp2_one(), fp2_zero()};
-  const uint32_t lo = off[b], hi_end = off[b + 1];
-  // both lanes of a pair run the same trip count (the pair's bucket)
+  if (pi >= MSM_NB * MSM_C) return;
+  const int b = pi / MSM_C, c = pi % MSM_C;
+  P2 R{fp2_zero(), fp2_one(), fp2_zero()};
+  const uint32_t end = off[b + 1];
+  uint32_t k = off[b] + c;
+  // the next point is in flight while this one is added (both lanes of a pair run the same trip count)
+  G2A q = sig[k < end ? lst[k] : 0u];
+  uint32_t li = k + MSM_C < end ? lst[k + MSM_C] : 0u;
 #pragma unroll 1
-  for (uint32_t k = lo; k < hi_end; ++k) {
-    const G2A& q = sig[lst[k]];
-    R = pp2_add_aff(R, q.x, q.y, hi);
+  for (; k < end; k += MSM_C) {
+    const G2A cq = q;
+    q = sig[li];
+    li = k + 2 * MSM_C < end ? lst[k + 2 * MSM_C] : 0u;
+    R = pp2_add_aff(R, cq.x, cq.y, hi);
   }
-  msm_store(bsum + (size_t)b * 6, R, hi);
+  p2_store(csum + (size_t)pi * 6, R, hi);
 }
 
-// out[j] = in[2j] + [2^k] in[2j+1] (k = 0: plain sum), one lane pair per output
-__global__ void __launch_bounds__(64) k_msm_tree2(const Fd* in, int nout, int k, Fd* out) {
-  const int t = blockIdx.x * 64 + threadIdx.x;
-  const int j = t >> 1;
-  const bool hi = (t & 1) != 0;
-  if (j >= nout) return;
-  const PP<Fp2> A = msm_load(in + (size_t)(2 * j) * 6);
-  PP<Fp2> Bp = msm_load(in + (size_t)(2 * j + 1) * 6);
+// U_b for b = blockIdx.x (w = b / 8, bit k = b % 8): lane pair j sums the MSM_C chunks of digit d_j (the j-th
+// digit with bit k set), then the 128 pair sums go through a 7-level LDS tree
+__global__ void __launch_bounds__(256) k_msm_usum(const Fp* csum, Fp* U) {
+  __shared__ Fp sm[128 * 6];
+  const int b = blockIdx.x, w = b >> 3, kb = b & 7;
+  const int j = threadIdx.x >> 1;
+  const bool hi = (threadIdx.x & 1) != 0;
+  const int d = ((j >> kb) << (kb + 1)) | (1 << kb) | (j & ((1 << kb) - 1));
+  const Fp* in = csum + (size_t)(w * 256 + d) * MSM_C * 6;
+  P2 R = p2_load(in);
 #pragma unroll 1
-  for (int s = 0; s < k; ++s) Bp = pp2_dbl(Bp, hi);
-  msm_store(out + (size_t)j * 6, pp2_add(A, Bp, hi), hi);
+  for (int c = 1; c < MSM_C; ++c) R = pp2_add(R, p2_load(in + 6 * c), hi);
+#pragma unroll 1
+  for (int s = 64; s >= 1; s >>= 1) {
+    if (j >= s && j < 2 * s) p2_store(sm + 6 * (j - s), R, hi);
+    __syncthreads();
+    if (j < s) R = pp2_add(R, p2_load(sm + 6 * j), hi);
+    __syncthreads();
+  }
+  if (j == 0) p2_store(U + 6 * b, R, hi);
 }
 
-// projective S -> affine (identity if Z = 0)
-__global__ void __launch_bounds__(64) k_msm_affine(const Fd* pt, G2A* out) {
-  __shared__ Fd s[WP_NCONST + WL_MA_STRIDE];
-  const int lane = threadIdx.x;
-  vm_load_consts(s);
-  const int item0 = WP_NCONST;
-  if (lane < 6) s[item0 + WL_MA_P + lane] = pt[lane];
-  __syncthreads();
-  vm_run<1>(VM_PROG(MA_NORM), s, item0, 0, nullptr);
-  if (lane == 0) s[item0 + WL_MA_NI] = fd_from_fp(fp_inv(fp_from_fd(s[item0 + WL_MA_N])));
-  __syncthreads();
-  vm_run<1>(VM_PROG(MA_INVFIN), s, item0, 0, nullptr);
-  vm_run<1>(VM_PROG(MA_TOAFF), s, item0, 0, nullptr);
-  if (lane == 0) {
+// S = sum_b 2^b U_b and its affine form: node j (< s) adds 2^s node_{j+s}, s = 32, 16, ..., 1 (node j of the
+// first level reads U_j and U_{j+32} from HBM); one workgroup of 32 lane pairs
+__global__ void __launch_bounds__(64) k_msm_weighted(const Fp* U, G2A* out) {
+  __shared__ Fp sm[32 * 6];
+  const int j = threadIdx.x >> 1;
+  const bool hi = (threadIdx.x & 1) != 0;
+  P2 R = p2_load(U + 6 * j);
+  P2 Bp = p2_load(U + 6 * (j + 32));
+#pragma unroll 1
+  for (int i = 0; i < 32; ++i) Bp = pp2_dbl(Bp, hi);
+  R = pp2_add(R, Bp, hi);
+#pragma unroll 1
+  for (int s = 16; s >= 1; s >>= 1) {
+    if (j >= s && j < 2 * s) p2_store(sm + 6 * (j - s), R, hi);
+    __syncthreads();
+    if (j < s) {
+      Bp = p2_load(sm + 6 * j);
+#pragma unroll 1
+      for (int i = 0; i < s; ++i) Bp = pp2_dbl(Bp, hi);
+      R = pp2_add(R, Bp, hi);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {  // (X : Y : Z) -> (X / Z, Y / Z); Z = 0 is the identity
     G2A r;
-    r.inf = fd_is_zero(s[item0 + WL_MA_N]);
-    r.x = Fp2{fp_from_fd(s[item0 + WL_MA_XY]), fp_from_fd(s[item0 + WL_MA_XY + 1])};
-    r.y = Fp2{fp_from_fd(s[item0 + WL_MA_XY + 2]), fp_from_fd(s[item0 + WL_MA_XY + 3])};
-    if (r.inf) r.x = r.y = fp2_zero();
+    r.inf = fp2_is_zero(R.z);
+    const Fp2 zi = fp2_inv_inline(R.z);
+    r.x = r.inf ? fp2_zero() : f2mul(R.x, zi);
+    r.y = r.inf ? fp2_zero() : f2mul(R.y, zi);
     *out = r;
   }
 }
 
 // Scratch: cnt[MSM_NB] | off[MSM_NB + 1] | cur[MSM_NB] (u32), lst[8 B] (u32);
-// points (Fd): bsum[MSM_NB * 6] | tree ping [64 * 128 * 6] | pong [64 * 64 * 6].
+// points (packed Fp, 6 per point, in units of Fd slots): chunk sums [MSM_NB * MSM_C] | U [64].
 size_t msm_scratch_u32(size_t B) { return (size_t)3 * MSM_NB + 1 + MSM_W * B; }
-size_t msm_scratch_fd() { return (size_t)MSM_NB * 6 + 64 * 128 * 6 + 64 * 64 * 6; }
+size_t msm_scratch_fd() { return ((size_t)(MSM_NB * MSM_C + 64) * 6 * sizeof(Fp) + sizeof(Fd) - 1) / sizeof(Fd); }
 
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc,
                       const G2A* sig, uint32_t* scr, Fd* pts, G2A* out) {
@@ -155,9 +194,8 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   uint32_t* off = cnt + MSM_NB;
   uint32_t* cur = off + MSM_NB + 1;
   uint32_t* lst = cur + MSM_NB;
-  Fd* bsum = pts;
-  Fd* ping = bsum + (size_t)MSM_NB * 6;
-  Fd* pong = ping + (size_t)64 * 128 * 6;
+  Fp* csum = reinterpret_cast<Fp*>(pts);
+  Fp* U = csum + (size_t)MSM_NB * MSM_C * 6;
   hipError_t e = hipMemsetAsync(cnt, 0, MSM_NB * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   const unsigned nb = (unsigned)((B * MSM_W + 255) / 256);
@@ -165,36 +203,17 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
     hipLaunchKernelGGL(k_msm_count, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(64), 0, st, cnt, off, cur);
+  hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(256), 0, st, cnt, off, cur);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (B) {
     hipLaunchKernelGGL(k_msm_scatter, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cur, lst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_msm_bucket2, dim3(2 * MSM_NB / 64), dim3(64), 0, st, off, lst, sig, bsum);
+  hipLaunchKernelGGL(k_msm_bucketc, dim3(2 * MSM_NB * MSM_C / 64), dim3(64), 0, st, off, lst, sig, csum);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_gather_bits, dim3(64 * 128 * 6 / 256), dim3(256), 0, st, bsum, ping);
+  hipLaunchKernelGGL(k_msm_usum, dim3(64), dim3(256), 0, st, csum, U);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  // U tree: 64 x 128 -> 64 (7 levels of pairwise sums; sets stay contiguous)
-  Fd* a = ping;
-  Fd* b = pong;
-  for (int n = 64 * 64; n >= 64; n >>= 1) {
-    hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, 0, b);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    Fd* t = a;
-    a = b;
-    b = t;
-  }
-  // weighted tree: sum_b 2^b U_b, 64 -> 1
-  int k = 1;
-  for (int n = 32; n >= 1; n >>= 1, k <<= 1) {
-    hipLaunchKernelGGL(k_msm_tree2, dim3((2 * n + 63) / 64), dim3(64), 0, st, a, n, k, b);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    Fd* t = a;
-    a = b;
-    b = t;
-  }
-  hipLaunchKernelGGL(k_msm_affine, dim3(1), dim3(64), 0, st, a, out);
+  hipLaunchKernelGGL(k_msm_weighted, dim3(1), dim3(64), 0, st, U, out);
   return hipGetLastError();
 }
 

@@ -135,3 +135,20 @@ extern "C" int hc_j2_add_aff(const uint8_t* p, const uint8_t* q, uint8_t* o) {
   return exc ? 1 : 0;
 }
 
+// register-resident hash_to_field of the FAV h2c kernel (bls_xmd32.h): 32-byte message, POP DST
+#include "bls_xmd32.h"
+extern "C" void hc_hash_to_field_m32(const uint8_t* m32, uint8_t* o) {
+  Fp2 u[2];
+  hash_to_field_fp2_m32(u, m32);
+  out_fp2(o, u[0]);
+  out_fp2(o + 96, u[1]);
+}
+// the inline SSWU of the FAV h2c kernel (bls_lane.h map_to_curve_sswu_lane_i); returns its `rare` flag
+extern "C" int hc_map_to_curve_lane_i(const uint8_t* u, uint8_t* o) {
+  Fp2 x, y;
+  bool rare = false;
+  map_to_curve_sswu_lane_i(x, y, in_fp2(u), rare);
+  out_fp2(o, x);
+  out_fp2(o + 96, y);
+  return rare ? 1 : 0;
+}

@@ -3,6 +3,7 @@
 Runs on CPU: it compiles the same headers the gfx950 kernels use for the host
 and compares every layer (Fp .. pairing, hash_to_G2, decode) with oracle/.
 """
+import hashlib
 import random
 
 import pytest
@@ -183,6 +184,13 @@ def test_expand_and_hash_to_field():
         assert [H.b_fp2(u[:96]), H.b_fp2(u[96:])] == O.hash_to_field_fp2(msg, 2, dst)
 
 
+def test_hash_to_field_m32_register_form():
+    """bls_xmd32.h (the FAV h2c kernel's expand_message_xmd with compile-time block constants) against the oracle."""
+    for msg in (bytes(32), b"\x12" * 32, b"\xff" * 32, bytes(range(32)), hashlib.sha256(b"m32").digest()):
+        u = H.call("hc_hash_to_field_m32", msg, out=192)
+        assert [H.b_fp2(u[:96]), H.b_fp2(u[96:])] == O.hash_to_field_fp2(msg, 2, O.DST_POP)
+
+
 def test_expand_message_rfc9380_vector():
     # RFC 9380 App. K.1 (expand_message_xmd SHA-256, DST QUUX-V01-CS02-with-expander-SHA256-128), msg="" len 0x20
     dst = b"QUUX-V01-CS02-with-expander-SHA256-128"
@@ -236,6 +244,10 @@ def test_lane_chain_math():
     for u in [rfp2() for _ in range(16)] + [(0, 0), (1, 0), (0, 1)]:
         out = H.call("hc_map_to_curve_lane", H.fp2_b(u), out=192)
         assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
+    # the inline form of the FAV h2c kernel: same point, `rare` only where g(x1) = 0 or g(x) lies in Fp
+    for u in [rfp2() for _ in range(16)] + [(0, 0), (1, 0), (0, 1)]:
+        rare, out = H.call("hc_map_to_curve_lane_i", H.fp2_b(u), out=192, ret=True)
+        assert rare == 0 and (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
     # decompression incl. both y signs
     for k in (1, 2, 3, 0xDEADBEEF, 0x5EED5EED):
         q = O.g2_mul(O.G2_GEN, k)
