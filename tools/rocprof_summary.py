@@ -9,6 +9,19 @@ import sqlite3
 import sys
 
 
+def _lib_sha():
+    """sha256 (16 hex) of the in-tree libblsmi355x.so that was profiled: bench.py reports the rocprof figures
+    only for the same build"""
+    import hashlib
+    import os
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "eth-consensus-specs_amd",
+                       "libblsmi355x.so")
+    try:
+        return hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def main(db, out=None, out_json=None, source=None):
     c = sqlite3.connect(db)
     rows = c.execute(
@@ -29,7 +42,8 @@ def main(db, out=None, out_json=None, source=None):
     if out_json:
         avg = {r[0].split("(")[0].replace("void ", "").replace("bls::", ""): round(r[3] / 1e6, 4) for r in rows}
         with open(out_json, "w") as fh:
-            json.dump({"source": source or out or db, "avg_ms": avg}, fh, indent=1, sort_keys=True)
+            json.dump({"source": source or out or db, "avg_ms": avg, "lib_sha256_16": _lib_sha()}, fh, indent=1,
+                      sort_keys=True)
     print(text)
 
 
