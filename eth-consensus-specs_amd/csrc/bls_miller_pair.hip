@@ -35,6 +35,13 @@ __device__ __forceinline__ uint32_t dpp_q(uint32_t v) {
 __device__ __forceinline__ uint32_t dpp_h(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
 }
+// quad broadcasts (lane 4k + 2h + q): the value of the q = 0 / q = 1 lane of the same h, of the h = 0 / h = 1 lane
+// of the same q -- one DPP move where an exchange plus a lane select took three instructions
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_b(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr int BQ0 = 0xA0, BQ1 = 0xF5, BH0 = 0x44, BH1 = 0xEE;  // quad_perm [0,0,2,2] [1,1,3,3] [0,1,0,1] [2,3,2,3]
 
 }  // namespace
 
@@ -92,6 +99,21 @@ template <uint64_t V, uint64_t D>
 __device__ __forceinline__ Fq6B<V, D> dh6(const Fq6B<V, D>& a) {
   return {dh2(a.c0), dh2(a.c1), dh2(a.c2)};
 }
+template <int CTRL, uint64_t V, uint64_t D>
+__device__ __forceinline__ FqB<V, D> bc(const FqB<V, D>& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = dpp_b<CTRL>(a.x.d[i]);
+  return {r};
+}
+template <int CTRL, uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq2B<V, D> bc2(const Fq2B<V, D>& a) {
+  return {bc<CTRL>(a.c0), bc<CTRL>(a.c1)};
+}
+template <int CTRL, uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq6B<V, D> bc6(const Fq6B<V, D>& a) {
+  return {bc2<CTRL>(a.c0), bc2<CTRL>(a.c1), bc2<CTRL>(a.c2)};
+}
 
 // X * Y in Fp6, three of its six Fp2 products on each q lane (as q6mul)
 template <uint64_t VX, uint64_t DX, uint64_t VY, uint64_t DY>
@@ -102,9 +124,8 @@ __device__ __forceinline__ auto qq6mul(const Fq6B<VX, DX>& X, const Fq6B<VY, DY>
   SEQ();
   const auto p2 = sel(q, norm(X.c0 + X.c2), X.c2) * sel(q, norm(Y.c0 + Y.c2), Y.c2);
   SEQ();
-  const auto o0 = dq2(p0), o1 = dq2(p1), o2 = dq2(p2);
-  const auto t0 = sel(q, o0, p0), t1 = sel(q, o1, p1), t2 = sel(q, o2, p2);
-  const auto u0 = sel(q, p0, o0), u1 = sel(q, p1, o1), u2 = sel(q, p2, o2);
+  const auto t0 = bc2<BQ0>(p0), t1 = bc2<BQ0>(p1), t2 = bc2<BQ0>(p2);  // the q = 0 lane's products
+  const auto u0 = bc2<BQ1>(p0), u1 = bc2<BQ1>(p1), u2 = bc2<BQ1>(p2);  // the q = 1 lane's
   const auto c0 = norm(xi(norm(u0 - (t1 + t2))) + t0);
   const auto c1 = norm((u1 - (t0 + t1)) + xi(t2));
   const auto c2 = norm((u2 - (t0 + t2)) + t1);
@@ -114,12 +135,11 @@ __device__ __forceinline__ auto qq6mul(const Fq6B<VX, DX>& X, const Fq6B<VY, DY>
 // one Fp12 squaring on the (h, q) lanes, as q_sqr
 template <uint64_t V, uint64_t D>
 __device__ __forceinline__ auto qq_sqr(const Fq6B<V, D>& own, bool h, bool q) {
-  const auto oth = dh6(own);
-  const auto A = sel(h, oth, own), Bv = sel(h, own, oth);
+  const auto A = bc6<BH0>(own), Bv = bc6<BH1>(own);  // a and b on every lane
   const auto X = norm(sel(h, A, A + Bv));
   const auto Y = norm(sel(h, Bv, A + f6v(Bv)));
   const auto P = qq6mul(X, Y, q);
-  const auto t = dh6(P);
+  const auto t = bc6<BH1>(P);  // a b (the h = 1 lanes' product)
   return norm(sel(h, P + P, (P - t) - f6v(t)));
 }
 
@@ -136,12 +156,11 @@ __device__ __forceinline__ auto qq_line(const Fq6B<V, D>& own, bool h, bool q, c
   SEQ();
   const auto p4 = sel(q, dh2(own.c1), own.c2) * sel(q, l3, l0);
   SEQ();
-  const auto o1 = dq2(p1), o2 = dq2(p2), o3 = dq2(p3), o4 = dq2(p4);
-  const auto t0 = sel(q, o1, p1), t1 = sel(q, o2, p2), u0 = sel(q, o3, p3), u2 = sel(q, o4, p4);
-  const auto u1 = sel(q, p1, o1), v0 = sel(q, p2, o2), v1 = sel(q, p3, o3), v2 = sel(q, p4, o4);
+  const auto t0 = bc2<BQ0>(p1), t1 = bc2<BQ0>(p2), u0 = bc2<BQ0>(p3), u2 = bc2<BQ0>(p4);  // q = 0 products
+  const auto u1 = bc2<BQ1>(p1), v0 = bc2<BQ1>(p2), v1 = bc2<BQ1>(p3), v2 = bc2<BQ1>(p4);  // q = 1 products
   const auto m01 = fq6b(t0 + xi(u0), (u1 - (t0 + t1)), t1 + u2);
   const auto m1 = fq6b(xi(v0), v1, v2);
-  return norm(norm(m01) + norm(sel(h, m1, f6v(m1))));
+  return norm(norm(m01) + sel(h, m1, f6v(m1)));
 }
 
 // one line's inputs on lane (h, q): l0 and the coefficient this lane scales (component q of E ZZ for h = 0, of
@@ -165,11 +184,9 @@ __device__ __forceinline__ void qq_line_p(const LineIn& in, const G1A* PP, bool 
                                           Fq2B<2, fqb_detail::MASK>& l3) {
   const FqC pc = fqb_canon(h ? PP->y : PP->x);
   const FqN mine = fqb_canon(in.c) * sel(h, pc, FqC{fq_zero()} - pc);  // -x_P as K - x_P (K a multiple of p)
-  const FqN part = dq(mine);
-  const Fq2B<2, fqb_detail::MASK> m{sel(q, part, mine), sel(q, mine, part)};
-  const auto o = dh2(m);
-  l2 = sel(h, o, m);
-  l3 = sel(h, m, o);
+  const Fq2B<2, fqb_detail::MASK> m{bc<BQ0>(mine), bc<BQ1>(mine)};  // (component 0, component 1) of this h's product
+  l2 = bc2<BH0>(m);                                                  // E ZZ (-x_P), from the h = 0 lanes
+  l3 = bc2<BH1>(m);                                                  // z3 ZZ y_P, from the h = 1 lanes
 }
 
 }  // namespace
