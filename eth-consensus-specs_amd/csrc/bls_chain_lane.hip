@@ -19,12 +19,17 @@ namespace bls {
 // hf staging layout of bls_fav_kernels.hip: HCF Fd slots per item, a projective
 // E2 point = 6 consecutive slots (X.c0, X.c1, Y.c0, Y.c1, Z.c0, Z.c1).
 
-// k_sig_lane with the G2 chain on lane pairs: blocks [0, nb1) run r_i apk_i
-// (one lane per item), blocks [nb1, nb1 + nb2) [|x|] sigma_i (two lanes per item).
+// blocks [0, nb) run r_i apk_i, blocks [nb, 2 nb) the G2 subgroup check of sigma_i, one lane per item each.
+// The subgroup check runs [|x|] sigma through the Jacobian digit-form chain (bls_fq_g2.h, 16 FME per doubling on
+// one lane instead of 2 x 12 on a lane pair with the complete formulas), the base point parked in LDS.  Its
+// additions are incomplete, which is exact here: an exceptional step (an intermediate equal to +-sigma or the
+// identity) means sigma has order below 2^64, so sigma is not in G2 (order r) and is rejected -- as is an
+// identity result.
 __global__ void __launch_bounds__(64) k_sig_lane2(size_t B, const int* gstat, int* status, const int* dstat,
                                                   const G1P* apk, const G2A* sig, const uint64_t* rsc, G1P* rPj) {
-  const unsigned nb1 = (unsigned)((B + 63) / 64);
-  if (blockIdx.x < nb1) {  // r_i apk_i in the redundant digit form (bls_fq_g1.h), canonical output
+  __shared__ uint32_t lds[84 * 64];
+  const unsigned nb = (unsigned)((B + 63) / 64);
+  if (blockIdx.x < nb) {  // r_i apk_i in the redundant digit form (bls_fq_g1.h), canonical output
     const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= B || !(gstat[i] && dstat[i])) return;
     const G1P a = apk[i];
@@ -40,33 +45,28 @@ __global__ void __launch_bounds__(64) k_sig_lane2(size_t B, const int* gstat, in
     rPj[i] = G1P{fq_pack(R.x), fq_pack(R.y), fq_pack(R.z)};
     return;
   }
-  const size_t t = (size_t)(blockIdx.x - nb1) * 64 + threadIdx.x;
-  const size_t i = t >> 1;
-  const bool hi = (t & 1) != 0;
-  if (i >= B) return;  // both lanes of an item leave together
+  const size_t i = (size_t)(blockIdx.x - nb) * 64 + threadIdx.x;
+  if (i >= B) return;
   if (!(gstat[i] && dstat[i])) {
-    if (!hi) status[i] = 0;
+    status[i] = 0;
     return;
   }
   const G2A s = sig[i];
-  PP<Fp2> M{s.x, s.y, fp2_one()};
-#pragma unroll 1
-  for (int b = 62; b >= 0; --b) {
-    M = pp2_dbl(M, hi);
-    if ((X_ABS >> b) & 1ull) M = pp2_add_aff(M, s.x, s.y, hi);
-  }
-  // sigma in G2  <=>  psi(sigma) == -M, M not the identity: lane 0 checks x, lane 1 y
-  const Fp2 pc = f2mul(fp2_conj(hi ? s.y : s.x), hi ? PSI_CY : PSI_CX);
-  const Fp2 d = hi ? fp2_add(f2mul(pc, M.z), M.y) : fp2_sub(f2mul(pc, M.z), M.x);
-  const uint32_t mine = fp2_is_zero(d) ? 1u : 0u;
-  const bool ok = mine && cl_swap(mine) && !fp2_is_zero(M.z);
-  if (!hi) status[i] = ok ? 1 : 0;
+  bool exc = false;
+  const J2Q M = j2q_mul_xabs_lds(J2Q{fq2_unpack(s.x), fq2_unpack(s.y), fq2_unpack(fp2_one())}, exc, lds);
+  // sigma in G2  <=>  psi(sigma) == -[|x|] sigma:  conj(x) CX Z^2 == X,  conj(y) CY Z^3 == -Y,  Z != 0
+  const Fp2 X = fq2_pack(M.x), Y = fq2_pack(M.y), Z = fq2_pack(M.z);
+  const Fp2 zz = f2sqr(Z);
+  const Fp2 px = f2mul(f2mul(fp2_conj(s.x), PSI_CX), zz);
+  const Fp2 py = f2mul(f2mul(fp2_conj(s.y), PSI_CY), f2mul(zz, Z));
+  const Fp2 dx = fp2_sub(px, X), dy = fp2_add(py, Y);
+  status[i] = (!exc && !fp2_is_zero(Z) && fp2_is_zero(dx) && fp2_is_zero(dy)) ? 1 : 0;
 }
 
 hipError_t launch_sig_lane(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat, const G1P* apk,
                            const G2A* sig, const uint64_t* rsc, G1P* rPj) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_lane2, dim3((unsigned)((B + 63) / 64 + (2 * B + 63) / 64)), dim3(64), 0, st, B, gstat,
+  hipLaunchKernelGGL(k_sig_lane2, dim3((unsigned)(2 * ((B + 63) / 64))), dim3(64), 0, st, B, gstat,
                      status, dstat, apk, sig, rsc, rPj);
   return hipGetLastError();
 }

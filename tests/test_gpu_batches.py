@@ -165,3 +165,54 @@ def test_aggregate_verify_many_messages(N):
     swapped[0], swapped[1] = swapped[1], swapped[0]
     assert shim.AggregateVerify(pkl, swapped, agg) is False
     assert OC.AggregateVerify(pkl[:128], msgs[:128], agg) is (N == 128)
+
+
+def _e2_point(x0):
+    """a point of E2(Fp2) with x = (x0, 1), any order"""
+    x = x0
+    while True:
+        X = (x, 1)
+        y = O.f2_sqrt(O.f2_add(O.f2_mul(O.f2_sqr(X), X), O.B2))
+        if y is not None:
+            return (X, y)
+        x += 1
+
+
+H2 = 0x5D543A95414E7F1091D50792876A202CD91DE4547085ABAA68A205B2E5A7DDFA628F1CB4D9E82EF21537E293A6691AE1616EC6E786F0C70CF1C38E31C7238E5
+
+
+def _small_order_e2(q):
+    """a point of E2 of order q for q = 13 or 23 (q^2 divides the G2 cofactor and E2's q-part has exponent q, so the
+    multiplier drops every factor q; None is the identity in the oracle)"""
+    x = 1
+    while True:
+        Q = O.g2_mul(_e2_point(x), H2 * O.R // (q * q))
+        if Q is not None:
+            assert O.g2_mul(Q, q) is None
+            return Q
+        x += 1
+
+
+def test_fav_batch_signatures_outside_g2(batch, registry):
+    """Signatures that decode to points of E2 outside G2 (the subgroup check): a random E2
+    point, and points of order 13 and 23 -- the small-order ones make the incomplete Jacobian [|x|] chain of
+    k_sig_lane2 hit its exceptional additions, which must reject.  Verdicts against the construction and the
+    C oracle, through the batch path and the per-call path."""
+    from bls_mi355x import bls as shim
+    shim.use_mi355x()
+    shim.bls_active = True
+    B, n = 6, 16
+    idx, offs, msgs, sigs = _make_batch(batch, B, n, seed=0xB2)
+    bad = {1: _e2_point(3), 2: _small_order_e2(13), 4: _small_order_e2(23)}
+    for j, pt in bad.items():
+        assert not O.g2_in_subgroup(pt)
+        sigs[96 * j: 96 * j + 96] = O.g2_compress(pt)
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+    expect = [j not in bad for j in range(B)]
+    assert out.tolist() == expect
+    idx2 = idx.reshape(B, n)
+    for j in range(B):
+        pks = [registry[48 * int(k): 48 * int(k) + 48] for k in idx2[j]]
+        sig = bytes(sigs[96 * j: 96 * j + 96])
+        assert OC.FastAggregateVerify(pks, msgs[j], sig) is expect[j]
+        assert shim.FastAggregateVerify(pks, msgs[j], sig) is expect[j]
