@@ -220,6 +220,15 @@ BLS_HD auto operator*(const Fq2B<V1, D1>& a, const Fq2B<V2, D2>& b) {
   return Fq2B<R::val, R::dig>{relax<R::val, R::dig>(c0), relax<R::val, R::dig>(c1)};
 }
 
+// complex squaring: (a0 + a1)(a0 - a1), 2 a0 a1
+template <uint64_t V, uint64_t D>
+BLS_HD auto sqr(const Fq2B<V, D>& a) {
+  const FqN t0 = (a.c0 + a.c1) * norm(a.c0 - a.c1);
+  const auto t1 = small<2>(FqN(a.c0 * a.c1));
+  using R = FqB<(decltype(t1)::val > 2 ? decltype(t1)::val : 2), decltype(t1)::dig>;
+  return Fq2B<R::val, R::dig>{relax<R::val, R::dig>(t0), relax<R::val, R::dig>(t1)};
+}
+
 // ---- Fp6 = Fp2[v]/(v^3 - xi) -----------------------------------------------
 template <uint64_t V, uint64_t D>
 struct Fq6B {

@@ -61,6 +61,11 @@ size_t msm_scratch_fd();
 hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
 // the same Miller values in two kernels (G2 lines, then f); L: miller_lines_u32(n) words of scratch
 constexpr int MILLER_NLINES = 68;  // 63 doublings + 5 additions (|x| = 0xd201000000010000)
+// Miller line records (k_miller_lines2 -> k_miller_acc4q): three Fp2 -- (l0, E ZZ, z3 ZZ) for a doubling, (l0, r,
+// z3) for an addition -- as 14-digit bound-typed values (bls_fqb.h FqB<ML_LV, ML_LD>: value < ML_LV p, digits <=
+// ML_LD), word w of line k of pair i at L[(k * ML_WORDS + w) * n + i]
+constexpr int ML_WORDS = 84;
+constexpr uint64_t ML_LV = 4096, ML_LD = 0x20000000ull + 64;
 size_t miller_lines_u32(size_t n);
 hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L);
 // four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values

@@ -9,71 +9,58 @@
 // 10,000-pair batch about 15 % of the chip for ~11 ms -- and the rest of the
 // GPU runs the other streams' kernels.  Per pair it is ~4.5x less SIMD time
 // than the wave-program version (tools/microbench/miller_lane.hip).
+#include "bls_fqb.h"
 #include "bls_kernels.h"
 #include "bls_tower_inline.h"
 
 namespace bls {
 
 
-// The same Miller loop in two kernels: the G2 side (doubling/addition steps of
-// T and the P-independent parts of the line coefficients) and the f
-// accumulation.  Each kernel holds about half of the fused kernel's live state
-// (T, Q and temporaries in the first; f and one line in the second), so the
-// spills of k_miller_lane go away.  Lines are stored unscaled --
-// (l0, E*ZZ, z3*ZZ) for a doubling, (l0, r, z3) for an addition -- and the
-// accumulation multiplies the last two by -x_P and y_P, exactly the products
-// ml_dbl_i / ml_add_i do, so the Miller values stay bit-identical.
-// Layout: word w of line k of pair i at L[(k * ML_WORDS + w) * n + i], so the
-// 64 lanes of a wave read and write 64 consecutive words.
-namespace {
-
-constexpr int ML_WORDS = 72;  // three Fp2 of 12 limbs each
-
-__device__ __forceinline__ void ml_store(uint32_t* L, size_t n, int w0, const Fp2& a) {
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    L[(size_t)(w0 + j) * n] = a.c0.l[j];
-    L[(size_t)(w0 + 12 + j) * n] = a.c1.l[j];
-  }
-}
-__device__ __forceinline__ Fp2 ml_load(const uint32_t* L, size_t n, int w0) {
-  Fp2 a;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    a.c0.l[j] = L[(size_t)(w0 + j) * n];
-    a.c1.l[j] = L[(size_t)(w0 + 12 + j) * n];
-  }
-  return a;
-}
-
-}  // namespace
-
-// The G2 side with TWO lanes per pair.  A doubling step of k_miller_lines is
-// 7 squarings + 4 products in Fp2 in three dependency levels; lanes 2k / 2k+1
-// split each level and exchange results by DPP (quad_perm [1,0,3,2]):
+// The Miller loop in two kernels: the G2 side here (doubling/addition steps of T and the P-independent parts of
+// the line coefficients) and the f accumulation (k_miller_acc4q, bls_miller_pair.hip).  Lines are stored unscaled
+// -- (l0, E*ZZ, z3*ZZ) for a doubling, (l0, r, z3) for an addition -- and the accumulation multiplies the last two
+// by -x_P and y_P.  Layout: word w of line k of pair i at L[(k * ML_WORDS + w) * n + i] (bls_kernels.h), so the
+// 64 lanes of a wave read and write consecutive words; the words are the 14 digits of bound-typed values
+// FqB<ML_LV, ML_LD> (bls_fqb.h), which the accumulation multiplies without unpacking.
+//
+// TWO lanes per pair.  A doubling step is 7 squarings + 4 products in Fp2 in three dependency levels; lanes
+// 2k / 2k+1 split each level and broadcast results by DPP:
 //   level 1   lane 0: A = x^2, ZZ = z^2          lane 1: B = y^2, YZ = (y + z)^2
 //   level 2   lane 0: C = B^2, XB = (x + B)^2,   lane 1: F = E^2, z3 ZZ, E ZZ
 //                     E x  (l0 = E x - 2B)       (E = 3A, z3 = YZ - B - ZZ)
 //   level 3   both: y3 = E (D - x3) - 8C         (D = 2(XB - A - C), x3 = F - 2D)
-// Each lane stores the line words it formed (lane 0: l0, lane 1: E ZZ and
-// z3 ZZ), so only C, XB and F cross lanes in level 2.  The five addition
-// steps run on both lanes (lane 0 stores l0, lane 1 the rest).  ~15 instead of
-// 26 FME per doubling and lane; the same canonical values as k_miller_lines.
+// Each lane stores the line words it formed (lane 0: l0, lane 1: E ZZ and z3 ZZ).  The five addition steps run on
+// both lanes (lane 0 stores l0, lane 1 the rest).  T stays in the bound-typed digit form for the whole loop
+// (declared FqB<LN_TV, LN_TD>; every step is relaxed to it, so its bounds are checked by induction at compile
+// time): no product unpacks or repacks, additions are digit-wise (the packed kernel: 12-limb carry chains and a
+// conditional subtraction per addition and per product).
+// products one after another (interleaved, their digit columns spilled ~140 VGPRs)
+#define LN_SEQ() __builtin_amdgcn_sched_barrier(0)
 namespace {
-__device__ __forceinline__ uint32_t ln_swap(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+constexpr uint64_t LN_TV = 1024, LN_TD = 0x20000000ull + 64;  // loop-carried bound of T's coordinates
+
+__device__ __forceinline__ uint32_t dpp_bc(uint32_t v, bool odd) {  // lane 2k's value (odd = false) or lane 2k+1's
+  return odd ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false)   // quad_perm [1,1,3,3]
+             : (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
 }
-__device__ __forceinline__ Fp2 ln_swap2(const Fp2& a) {
-  Fp2 r;
+template <bool ODD, uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq2B<V, D> bcp(const Fq2B<V, D>& a) {
+  Fq2B<V, D> r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    r.c0.l[i] = ln_swap(a.c0.l[i]);
-    r.c1.l[i] = ln_swap(a.c1.l[i]);
+  for (int i = 0; i < 14; i++) {
+    r.c0.x.d[i] = dpp_bc(a.c0.x.d[i], ODD);
+    r.c1.x.d[i] = dpp_bc(a.c1.x.d[i], ODD);
   }
   return r;
 }
-__device__ __forceinline__ Fp2 ln_sel2(bool c, const Fp2& a, const Fp2& b) {
-  return Fp2{fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)};
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ void ml_store_q(uint32_t* L, size_t n, int w0, const Fq2B<V, D>& v) {
+  const Fq2B<ML_LV, ML_LD> a = relax<ML_LV, ML_LD>(v);
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    L[(size_t)(w0 + j) * n] = a.c0.x.d[j];
+    L[(size_t)(w0 + 14 + j) * n] = a.c1.x.d[j];
+  }
 }
 }  // namespace
 
@@ -84,75 +71,101 @@ __global__ void __launch_bounds__(64) k_miller_lines2(const G2A* Q, size_t n, ui
   if (i >= n) return;  // both lanes of a pair leave together
   const G2A q = Q[i];
   if (q.inf) return;
-  G2J T{q.x, q.y, fp2_one()};
+  using TF = Fq2B<LN_TV, LN_TD>;
+  using QF = Fq2B<1, fqb_detail::MASK>;
+  // Q's coordinates wait in LDS ([word][lane]) for the five addition steps: held in registers across the 63
+  // doublings they pushed the kernel into spills
+  __shared__ uint32_t qlds[56 * 64];
+  {
+    const QF qx = fq2b_canon(q.x), qy = fq2b_canon(q.y);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&qx);
+    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&qy);
+#pragma unroll
+    for (int k = 0; k < 28; k++) {
+      qlds[k * 64 + threadIdx.x] = w[k];
+      qlds[(28 + k) * 64 + threadIdx.x] = w2[k];
+    }
+  }
+  const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
+  TF X = relax<LN_TV, LN_TD>(fq2b_canon(q.x)), Y = relax<LN_TV, LN_TD>(fq2b_canon(q.y));
+  TF Z = relax<LN_TV, LN_TD>(QF{one, zero});
   uint32_t* Li = L + i;
   const size_t step = (size_t)ML_WORDS * n;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     {
-      // level 1: lane 0 squares x and z, lane 1 y and y + z
-      const Fp2 s0 = f2sqr(ln_sel2(hi, T.y, T.x));
-      const Fp2 s1 = f2sqr(ln_sel2(hi, f2add(T.y, T.z), T.z));
-      const Fp2 o0 = ln_swap2(s0), o1 = ln_swap2(s1);
-      const Fp2 A = ln_sel2(hi, o0, s0), ZZ = ln_sel2(hi, o1, s1);
-      const Fp2 Bq = ln_sel2(hi, s0, o0), YZ = ln_sel2(hi, s1, o1);
-      const Fp2 E = f2add(fp2_dbl(A), A);
-      const Fp2 z3 = f2sub(f2sub(YZ, Bq), ZZ);
-      // level 2: lane 0: C = B^2, XB = (x + B)^2, E x;  lane 1: F = E^2, E ZZ, z3 ZZ
-      const Fp2 r0 = f2sqr(ln_sel2(hi, E, Bq));                        // lane 0: C;   lane 1: F
-      const Fp2 xb = f2add(T.x, Bq);
-      const Fp2 r1 = f2mul(ln_sel2(hi, z3, xb), ln_sel2(hi, ZZ, xb));  // lane 0: XB;  lane 1: z3 ZZ
-      const Fp2 r2 = f2mul(E, ln_sel2(hi, ZZ, T.x));                   // lane 0: E x; lane 1: E ZZ
-      // stores: lane 0 l0 (words 0..23), lane 1 E ZZ (24..47) and z3 ZZ (48..71)
-      {
-        const Fp2 w0 = ln_sel2(hi, r2, f2sub(r2, fp2_dbl(Bq)));
-        uint32_t* o = Li + (size_t)(hi ? 24 : 0) * n;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) {
-          o[(size_t)j * n] = w0.c0.l[j];
-          o[(size_t)(12 + j) * n] = w0.c1.l[j];
-        }
-        if (hi) {
-#pragma unroll
-          for (int j = 0; j < 12; ++j) {
-            Li[(size_t)(48 + j) * n] = r1.c0.l[j];
-            Li[(size_t)(60 + j) * n] = r1.c1.l[j];
-          }
-        }
-      }
-      const Fp2 p0 = ln_swap2(r0), p1 = ln_swap2(r1);
-      const Fp2 C = ln_sel2(hi, p0, r0), XB = ln_sel2(hi, p1, r1), F = ln_sel2(hi, r0, p0);
-      // level 3 (both lanes)
-      const Fp2 D = fp2_dbl(f2sub(f2sub(XB, A), C));
-      const Fp2 x3 = f2sub(F, fp2_dbl(D));
-      const Fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
-      T.y = f2sub(f2mul(E, f2sub(D, x3)), C8);
-      T.x = x3;
-      T.z = z3;
+      const auto s0 = sqr(sel(hi, Y, X));
+      LN_SEQ();
+      const auto s1 = sqr(sel(hi, norm(Y + Z), Z));
+      LN_SEQ();
+      const auto A = bcp<false>(s0);
+      const auto Bq = bcp<true>(s0);
+      const auto ZZ = bcp<false>(s1);
+      const auto YZ = bcp<true>(s1);
+      const auto E = small<3>(A);
+      const auto z3 = norm(YZ - (Bq + ZZ));
+      const auto r0 = sqr(sel(hi, E, Bq));                        // lane 0: C;   lane 1: F
+      LN_SEQ();
+      const auto xb = norm(X + Bq);
+      const auto r1 = sel(hi, z3, xb) * sel(hi, ZZ, xb);          // lane 0: XB;  lane 1: z3 ZZ
+      LN_SEQ();
+      const auto r2 = E * sel(hi, ZZ, X);                         // lane 0: E x; lane 1: E ZZ
+      LN_SEQ();
+      ml_store_q(Li, n, hi ? 28 : 0, sel(hi, r2, norm(r2 - small<2>(Bq))));  // lane 0: l0 = E x - 2B
+      LN_SEQ();
+      if (hi) ml_store_q(Li, n, 56, r1);
+      LN_SEQ();
+      const auto C = bcp<false>(r0);
+      const auto XB = bcp<false>(r1);
+      const auto F = bcp<true>(r0);
+      const auto D = small<2>(norm(XB - (A + C)));
+      const auto x3 = norm(F - small<2>(D));
+      const auto y3 = norm(E * norm(D - x3) - small<8>(C));
+      LN_SEQ();
+      X = relax<LN_TV, LN_TD>(x3);
+      Y = relax<LN_TV, LN_TD>(y3);
+      Z = relax<LN_TV, LN_TD>(z3);
       Li += step;
     }
-    if ((X_ABS >> b) & 1ull) {  // addition step on both lanes (as k_miller_lines)
-      const Fp2 z1z1 = f2sqr(T.z);
-      const Fp2 u2 = f2mul(q.x, z1z1);
-      const Fp2 s2 = f2mul(f2mul(q.y, T.z), z1z1);
-      const Fp2 h = f2sub(u2, T.x);
-      const Fp2 hh = f2sqr(h);
-      const Fp2 i4 = fp2_dbl(fp2_dbl(hh));
-      const Fp2 j = f2mul(h, i4);
-      const Fp2 r = fp2_dbl(f2sub(s2, T.y));
-      const Fp2 v = f2mul(T.x, i4);
-      const Fp2 x3 = f2sub(f2sub(f2sqr(r), j), fp2_dbl(v));
-      const Fp2 y3 = f2sub(f2mul(r, f2sub(v, x3)), fp2_dbl(f2mul(T.y, j)));
-      const Fp2 z3 = f2sub(f2sub(f2sqr(f2add(T.z, h)), z1z1), hh);
-      if (hi) {
-        ml_store(Li, n, 24, r);
-        ml_store(Li, n, 48, z3);
-      } else {
-        ml_store(Li, n, 0, f2sub(f2mul(r, q.x), f2mul(q.y, z3)));
+    if ((X_ABS >> b) & 1ull) {  // addition step on both lanes (T + Q, Q affine)
+      QF qx, qy;
+      uint32_t* w = reinterpret_cast<uint32_t*>(&qx);
+      uint32_t* w2 = reinterpret_cast<uint32_t*>(&qy);
+#pragma unroll
+      for (int k = 0; k < 28; k++) {
+        w[k] = qlds[k * 64 + threadIdx.x];
+        w2[k] = qlds[(28 + k) * 64 + threadIdx.x];
       }
-      T.x = x3;
-      T.y = y3;
-      T.z = z3;
+      const auto z1z1 = sqr(Z);
+      LN_SEQ();
+      const auto u2 = qx * z1z1;
+      LN_SEQ();
+      const auto s2 = (qy * Z) * z1z1;
+      LN_SEQ();
+      const auto h = norm(u2 - X);
+      const auto hh = sqr(h);
+      LN_SEQ();
+      const auto i4 = small<4>(hh);
+      const auto j = h * i4;
+      LN_SEQ();
+      const auto r = small<2>(norm(s2 - Y));
+      const auto v = X * i4;
+      LN_SEQ();
+      const auto x3 = norm(sqr(r) - (j + small<2>(v)));
+      LN_SEQ();
+      const auto y3 = norm(r * norm(v - x3) - small<2>(Y * j));
+      LN_SEQ();
+      const auto z3 = norm(sqr(norm(Z + h)) - (z1z1 + hh));
+      LN_SEQ();
+      if (hi) {
+        ml_store_q(Li, n, 28, r);
+        ml_store_q(Li, n, 56, z3);
+      } else {
+        ml_store_q(Li, n, 0, norm(r * qx - qy * z3));
+      }
+      X = relax<LN_TV, LN_TD>(x3);
+      Y = relax<LN_TV, LN_TD>(y3);
+      Z = relax<LN_TV, LN_TD>(z3);
       Li += step;
     }
   }

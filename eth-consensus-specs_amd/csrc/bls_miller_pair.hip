@@ -9,20 +9,9 @@ namespace bls {
 
 namespace {
 
-constexpr int ML_WORDS2 = 72;  // line record: three Fp2 (l0, E*ZZ or r, z3*ZZ or z3), as k_miller_lines2 writes
 // loop-carried bound of the digit-form f halves: value < ML_QF_V p, digits <= ML_QF_D (every step's output is
 // relaxed to it at compile time: qq_sqr ends below 211 p, qq_line below ML_QF_V p)
 constexpr uint64_t ML_QF_V = 256, ML_QF_D = 0x20000000ull + 64;
-
-__device__ __forceinline__ Fp2 ml_load2(const uint32_t* L, size_t n, int w0) {
-  Fp2 a;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    a.c0.l[j] = L[(size_t)(w0 + j) * n];
-    a.c1.l[j] = L[(size_t)(w0 + 12 + j) * n];
-  }
-  return a;
-}
 
 // The Fp2 products of each Fp6 product run one after another (sched_barrier): letting the scheduler
 // interleave them held too many products live and spilled (the packed-form kernel measured 5.0 ms per
@@ -167,15 +156,19 @@ __device__ __forceinline__ auto qq_line(const Fq6B<V, D>& own, bool h, bool q, c
 // z3 ZZ for h = 1).  (Loading them one line ahead of use measured 3.72 ms per launch against 3.68 ms without, and
 // the 512-register allocation it needed cost ~15 % of pipelined throughput.)
 struct LineIn {
-  Fp2 l0;
-  Fp c;
+  Fq2B<ML_LV, ML_LD> l0;
+  FqB<ML_LV, ML_LD> c;
 };
 __device__ __forceinline__ LineIn ld_line(const uint32_t* Li, size_t n, bool h, bool q) {
   LineIn r;
-  r.l0 = ml_load2(Li, n, 0);
-  const int w0 = (h ? 48 : 24) + (q ? 12 : 0);
 #pragma unroll
-  for (int j = 0; j < 12; ++j) r.c.l[j] = Li[(size_t)(w0 + j) * n];
+  for (int j = 0; j < 14; ++j) {
+    r.l0.c0.x.d[j] = Li[(size_t)j * n];
+    r.l0.c1.x.d[j] = Li[(size_t)(14 + j) * n];
+  }
+  const int w0 = (h ? 56 : 28) + (q ? 14 : 0);
+#pragma unroll
+  for (int j = 0; j < 14; ++j) r.c.x.d[j] = Li[(size_t)(w0 + j) * n];
   return r;
 }
 
@@ -183,7 +176,7 @@ __device__ __forceinline__ LineIn ld_line(const uint32_t* Li, size_t n, bool h, 
 __device__ __forceinline__ void qq_line_p(const LineIn& in, const G1A* PP, bool h, bool q, Fq2B<2, fqb_detail::MASK>& l2,
                                           Fq2B<2, fqb_detail::MASK>& l3) {
   const FqC pc = fqb_canon(h ? PP->y : PP->x);
-  const FqN mine = fqb_canon(in.c) * sel(h, pc, FqC{fq_zero()} - pc);  // -x_P as K - x_P (K a multiple of p)
+  const FqN mine = in.c * sel(h, pc, FqC{fq_zero()} - pc);  // -x_P as K - x_P (K a multiple of p)
   const Fq2B<2, fqb_detail::MASK> m{bc<BQ0>(mine), bc<BQ1>(mine)};  // (component 0, component 1) of this h's product
   l2 = bc2<BH0>(m);                                                  // E ZZ (-x_P), from the h = 0 lanes
   l3 = bc2<BH1>(m);                                                  // z3 ZZ y_P, from the h = 1 lanes
@@ -218,7 +211,7 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
   }
   constexpr uint64_t VF = ML_QF_V, DF = ML_QF_D;
   using F = Fq6B<VF, DF>;
-  const size_t step = (size_t)ML_WORDS2 * n;
+  const size_t step = (size_t)ML_WORDS * n;
   const uint32_t* Lb[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) Lb[g] = L + pi[g];
@@ -236,7 +229,7 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
         const LineIn cur = ld_line(Lb[g], n, h, q);
         Fq2B<2, fqb_detail::MASK> l2, l3;
         qq_line_p(cur, P + pi[g], h, q, l2, l3);
-        const auto fl = relax<VF, DF>(qq_line(f, h, q, fq2b_canon(cur.l0), l2, l3));
+        const auto fl = relax<VF, DF>(qq_line(f, h, q, cur.l0, l2, l3));
         f = G == 1 ? fl : sel(live[g], fl, f);
         Lb[g] += step;
       }
