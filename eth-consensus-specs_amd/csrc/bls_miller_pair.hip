@@ -173,10 +173,10 @@ __device__ __forceinline__ LineIn ld_line(const uint32_t* Li, size_t n, bool h, 
 }
 
 // the line's P factors, as q_line_p: l2 = E ZZ (-x_P), l3 = z3 ZZ y_P in N form
-__device__ __forceinline__ void qq_line_p(const LineIn& in, const G1A* PP, bool h, bool q, Fq2B<2, fqb_detail::MASK>& l2,
+template <uint64_t VP, uint64_t DP>
+__device__ __forceinline__ void qq_line_p(const LineIn& in, const FqB<VP, DP>& pc, bool q, Fq2B<2, fqb_detail::MASK>& l2,
                                           Fq2B<2, fqb_detail::MASK>& l3) {
-  const FqC pc = fqb_canon(h ? PP->y : PP->x);
-  const FqN mine = in.c * sel(h, pc, FqC{fq_zero()} - pc);  // -x_P as K - x_P (K a multiple of p)
+  const FqN mine = in.c * pc;
   const Fq2B<2, fqb_detail::MASK> m{bc<BQ0>(mine), bc<BQ1>(mine)};  // (component 0, component 1) of this h's product
   l2 = bc2<BH0>(m);                                                  // E ZZ (-x_P), from the h = 0 lanes
   l3 = bc2<BH1>(m);                                                  // z3 ZZ y_P, from the h = 1 lanes
@@ -218,6 +218,10 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
   const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
   const Fq2B<1, fqb_detail::MASK> z2{zero, zero};
   F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
+  // the P coordinate each lane scales its line coefficient by: -x_P (h = 0, as K - x_P) or y_P (h = 1), once
+  // (two named values, not an array: the pair loop is not unrolled and an indexed array went to scratch)
+  const FqC pa = fqb_canon(h ? P[pi[0]].y : P[pi[0]].x), pb = fqb_canon(h ? P[pi[G - 1]].y : P[pi[G - 1]].x);
+  const auto pc0 = sel(h, pa, zero - pa), pc1 = sel(h, pb, zero - pb);
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = relax<VF, DF>(qq_sqr(f, h, q));
@@ -228,7 +232,7 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
       for (int g = 0; g < G; ++g) {
         const LineIn cur = ld_line(Lb[g], n, h, q);
         Fq2B<2, fqb_detail::MASK> l2, l3;
-        qq_line_p(cur, P + pi[g], h, q, l2, l3);
+        qq_line_p(cur, sel(g == 0, pc0, pc1), q, l2, l3);
         const auto fl = relax<VF, DF>(qq_line(f, h, q, cur.l0, l2, l3));
         f = G == 1 ? fl : sel(live[g], fl, f);
         Lb[g] += step;
