@@ -13,6 +13,7 @@
 #include "bls_pp_lane.h"
 #include "bls_vm.h"
 #include "bls_xmd32.h"
+#include "bls_fp_inv.h"
 
 namespace bls {
 
@@ -101,7 +102,7 @@ __global__ void __launch_bounds__(64) k_g1_affine_b(size_t B, const int* status,
     acc = fp_mul_i(acc, zero[k] ? FP_ONE : z);
     pre[k] = acc;
   }
-  Fp inv = fp_inv_i(acc);  // 1 / (z_0 ... z_{K-1})
+  Fp inv = fp_inv_sg_i(acc);  // 1 / (z_0 ... z_{K-1})
 #pragma unroll
   for (int k = AFF_K - 1; k >= 0; --k) {
     const size_t i = base + 64 * k;
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(64) k_h2c_affine_b(size_t B, const int* status
     acc = fp_mul_i(acc, zero[k] ? FP_ONE : n);
     pre[k] = acc;
   }
-  Fp inv = fp_inv_i(acc);
+  Fp inv = fp_inv_sg_i(acc);
 #pragma unroll
   for (int k = AFF_K - 1; k >= 0; --k) {
     const size_t i = base + 64 * k;

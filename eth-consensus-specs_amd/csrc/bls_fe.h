@@ -142,7 +142,7 @@ BLS_HD void fe_lin32(FeSlot* s, const uint32_t* w, int a, int b, int d) {
 
 BLS_HD void fe_inv(FeSlot* s, const uint32_t* w, int a, int b, int d) {
   const Fp v = fq_pack(fe_ld(s, fe_addr(fe_term(w, 0), a, b, d)));  // canonical
-  fe_st(s, fe_addr(w[0] & 1023u, a, b, d), fq_unpack(fp_inv_sg(v)));
+  fe_st(s, fe_addr(w[0] & 1023u, a, b, d), fq_unpack(fp_inv_sg_i(v)));
 }
 
 // one lane's part of a phase (its descriptor words w); KIND (bits 29..31): 1 PROD, 2 LIN, 3 INV, 4 LIN32 (idle

@@ -254,79 +254,6 @@ BLS_HD void raw_sub(Fp& a, const Fp& b) {
   }
 }
 BLS_HD bool raw_geq(const Fp& a, const Fp& b) { return !raw_lt(a.l, b.l); }
-// x / 2 mod p for x < p
-BLS_HD void half_mod_p(Fp& x) {
-  if (raw_is_even(x)) {
-    raw_shr1(x, 0);
-    return;
-  }
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)x.l[i] + P_LIMBS[i] + c;
-    x.l[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
-  raw_shr1(x, c);
-}
-
-// Inverse in Montgomery form: (aR)^-1 by binary extended Euclid on the raw
-// residue, then * R^3 / R.  ~2*381 shift/subtract steps instead of the 570
-// Montgomery multiplications of Fermat.  0 maps to 0.
-BLS_HDNI Fp fp_inv(const Fp& a) {
-  if (fp_is_zero(a)) return a;
-  Fp u = a, v, x1 = fp_zero(), x2 = fp_zero();
-#pragma unroll
-  for (int i = 0; i < 12; i++) v.l[i] = P_LIMBS[i];
-  x1.l[0] = 1;
-  while (!raw_is_one(u) && !raw_is_one(v)) {
-    while (raw_is_even(u)) {
-      raw_shr1(u, 0);
-      half_mod_p(x1);
-    }
-    while (raw_is_even(v)) {
-      raw_shr1(v, 0);
-      half_mod_p(x2);
-    }
-    if (raw_geq(u, v)) {
-      raw_sub(u, v);
-      x1 = fp_sub(x1, x2);
-    } else {
-      raw_sub(v, u);
-      x2 = fp_sub(x2, x1);
-    }
-  }
-  Fp r = raw_is_one(u) ? x1 : x2;
-  return fp_mul(r, FP_R3);
-}
-
-// fp_inv inline (the lane kernels on per-job streams: an out-of-line call costs the kernel a private segment)
-BLS_HD Fp fp_inv_i(const Fp& a) {
-  if (fp_is_zero(a)) return a;
-  Fp u = a, v, x1 = fp_zero(), x2 = fp_zero();
-#pragma unroll
-  for (int i = 0; i < 12; i++) v.l[i] = P_LIMBS[i];
-  x1.l[0] = 1;
-  while (!raw_is_one(u) && !raw_is_one(v)) {
-    while (raw_is_even(u)) {
-      raw_shr1(u, 0);
-      half_mod_p(x1);
-    }
-    while (raw_is_even(v)) {
-      raw_shr1(v, 0);
-      half_mod_p(x2);
-    }
-    if (raw_geq(u, v)) {
-      raw_sub(u, v);
-      x1 = fp_sub(x1, x2);
-    } else {
-      raw_sub(v, u);
-      x2 = fp_sub(x2, x1);
-    }
-  }
-  return fp_mul_i(raw_is_one(u) ? x1 : x2, FP_R3);
-}
-
 BLS_HDNI Fp fp_inv_fermat(const Fp& a) { return fp_pow(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
 
 BLS_HD bool fp_is_one(const Fp& a) { return fp_eq(a, FP_ONE); }
@@ -416,3 +343,6 @@ BLS_HDNI bool fp_is_square_euler(const Fp& a) {
 }
 
 }  // namespace bls
+
+// fp_inv (Bernstein-Yang divsteps) needs the definitions above
+#include "bls_fp_inv.h"

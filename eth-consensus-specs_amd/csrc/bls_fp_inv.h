@@ -206,8 +206,9 @@ BLS_HD Fp sg_to_fp(const S62& x) {  // x in [0, p)
   return r;
 }
 
-// Plain modular inverse of the integer a (canonical, < p); 0 -> 0
-BLS_HDNI Fp fp_inv_plain_sg(const Fp& a) {
+// Plain modular inverse of the integer a (canonical, < p); 0 -> 0.  Inline form for the lane kernels (an
+// out-of-line call gives the kernel a private segment); fp_inv_plain_sg is the out-of-line one.
+BLS_HD Fp fp_inv_plain_sg_i(const Fp& a) {
   S62 f{}, g = sg_from_fp(a), d{}, e{};
 #pragma unroll
   for (int i = 0; i < 7; i++) f.v[i] = SG.p[i];
@@ -226,7 +227,13 @@ BLS_HDNI Fp fp_inv_plain_sg(const Fp& a) {
   return sg_to_fp(d);
 }
 
+BLS_HDNI Fp fp_inv_plain_sg(const Fp& a) { return fp_inv_plain_sg_i(a); }
+
 // Montgomery-form inverse, as fp_inv: (a R)^-1 R^3 / R = a^-1 R
 BLS_HD Fp fp_inv_sg(const Fp& a) { return fp_mul(fp_inv_plain_sg(a), FP_R3); }
+BLS_HD Fp fp_inv_sg_i(const Fp& a) { return fp_mul_i(fp_inv_plain_sg_i(a), FP_R3); }
+// the general Montgomery-form inverse (0 -> 0).  It replaced a bit-serial binary extended Euclid whose
+// data-dependent branches diverged across the lanes of the batch kernels (~170k VALU instructions per inverse).
+BLS_HDNI Fp fp_inv(const Fp& a) { return fp_mul(fp_inv_plain_sg_i(a), FP_R3); }
 
 }  // namespace bls

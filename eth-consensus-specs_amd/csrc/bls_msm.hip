@@ -20,6 +20,7 @@
 // launches: ~6.8 ms per C2 batch.)
 #include "bls_kernels.h"
 #include "bls_pp_lane.h"
+#include "bls_fp_inv.h"
 
 #include <stdlib.h>
 
@@ -96,7 +97,7 @@ __device__ __forceinline__ void p2_store(Fp* o, const P2& p, bool hi) {  // sele
 // 1 / (a0 + a1 i) = (a0 - a1 i) / (a0^2 + a1^2) with the inline Fp inverse (an out-of-line call here cost a
 // 960-B private segment on the job's stream)
 __device__ __forceinline__ Fp2 fp2_inv_inline(const Fp2& a) {
-  const Fp ni = fp_inv_i(fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1)));
+  const Fp ni = fp_inv_sg_i(fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1)));
   return Fp2{fp_mul_i(a.c0, ni), fp_neg(fp_mul_i(a.c1, ni))};
 }
 __device__ __forceinline__ P2 p2_load(const Fp* in) {
