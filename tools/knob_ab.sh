@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of env knobs: each argument is a space-separated "VAR=VALUE ..." set (or "base").  The sets run
 # interleaved REPS times (default 3), STEPS timed passes each (default 60); the median per set is printed.
-# Usage (via gpurun): REPS=3 bash tools/knob_ab.sh TAG "base" "BLS_XC_G=1" ...
+# Usage (via gpurun): REPS=3 bash tools/knob_ab.sh TAG "base" "BLS_FAV_JOBS_INIT=6" ...
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
