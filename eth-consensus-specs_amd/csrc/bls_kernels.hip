@@ -496,9 +496,10 @@ hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, ui
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const RegKey* reg,
                              uint32_t reg_n, G1P* apk, int* status) {
   if (!B) return hipSuccess;
-  // lanes per aggregate: 16 while that still gives >= ~2 waves per SIMD and the
-  // committees are not huge (the per-lane chains stay short), else 64
-  if (B >= 8192)
+  // lanes per aggregate: 16 from 1,024 aggregates up (C2 and the C3 epoch of 2,048: 32 mixed additions per lane and
+  // a 4-level tree beat 8 + 6 levels of 64 lanes -- C3 +4 %, profiles/r03u_inv_gather_ab.txt), else 64 (a few
+  // aggregates spread over more lanes: shorter chains)
+  if (B >= 1024)
     LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else
     LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
