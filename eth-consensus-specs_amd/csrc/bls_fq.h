@@ -54,6 +54,10 @@ inline void fq_check_mul(const Fq& x, const Fq& y) {
   assert(fq_check_top(x) * fq_check_top(y) < 13.0 * __builtin_ldexp(1.0, 29));
 }
 #define FQ_CHECK_MUL(x, y) fq_check_mul(x, y)
+inline void fq_check_dot2(const Fq& x, const Fq& y, const Fq& u, const Fq& v) {
+  assert(fq_check_top(x) * fq_check_top(y) + fq_check_top(u) * fq_check_top(v) < 13.0 * __builtin_ldexp(1.0, 29));
+}
+#define FQ_CHECK_DOT2(x, y, u, v) fq_check_dot2(x, y, u, v)
 #define FQ_CHECK_COL(acc128) assert((acc128) < ((unsigned __int128)1 << 64))
 #define FQ_CHECK_SUB(b, K)                                        \
   do {                                                            \
@@ -61,6 +65,7 @@ inline void fq_check_mul(const Fq& x, const Fq& y) {
   } while (0)
 #else
 #define FQ_CHECK_MUL(x, y) ((void)0)
+#define FQ_CHECK_DOT2(x, y, u, v) ((void)0)
 #define FQ_CHECK_COL(acc128) ((void)0)
 #define FQ_CHECK_SUB(b, K) ((void)0)
 #endif
@@ -146,6 +151,57 @@ BLS_HD Fq fq_mul(const Fq& x, const Fq& y) {
         acc += (uint64_t)x.d[i] * y.d[j];
 #ifdef BLS_FQ_CHECK
         chk += (unsigned __int128)x.d[i] * y.d[j];
+#endif
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 1 && j < 14 && i < k) {
+        acc += (uint64_t)m[i] * P29[j];
+#ifdef BLS_FQ_CHECK
+        chk += (unsigned __int128)m[i] * P29[j];
+#endif
+      }
+    }
+    if (k < 14) {
+      m[k] = ((uint32_t)acc * P29_NINV) & Q29_MASK;
+      acc += (uint64_t)m[k] * P29[0];
+#ifdef BLS_FQ_CHECK
+      chk += (unsigned __int128)m[k] * P29[0];
+#endif
+    } else {
+      r.d[k - 14] = (uint32_t)acc & Q29_MASK;
+    }
+    FQ_CHECK_COL(chk);
+    acc >>= 29;
+  }
+  r.d[13] = (uint32_t)acc;
+  return r;
+}
+
+// Montgomery (x y + u v) / 2^406 with ONE reduction: both digit products of a column go into the same accumulator
+// ahead of the reduction products (28 + 14 terms).  N form, value < 2p when x y + u v < p R.  Karatsuba's
+// three products, two subtractions and two normalisations for an Fp2 product become two of these
+// (a0 b0 + a1 (-b1), a0 b1 + a1 b0) on a negation K - b1 (bls_fqb.h).
+BLS_HD Fq fq_mul_dot2(const Fq& x, const Fq& y, const Fq& u, const Fq& v) {
+  FQ_CHECK_DOT2(x, y, u, v);
+  uint32_t m[14];
+  Fq r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+#ifdef BLS_FQ_CHECK
+    unsigned __int128 chk = acc;
+#endif
+#pragma unroll
+    for (int i = 0; i < 14; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 14) {
+        acc += (uint64_t)x.d[i] * y.d[j];
+        acc += (uint64_t)u.d[i] * v.d[j];
+#ifdef BLS_FQ_CHECK
+        chk += (unsigned __int128)x.d[i] * y.d[j] + (unsigned __int128)u.d[i] * v.d[j];
 #endif
       }
     }

@@ -11,6 +11,7 @@
 // 128-bit column, value and subtraction checks of bls_fq.h compiled in.
 #pragma once
 #include "bls_fq.h"
+#include "bls_fqb.h"
 #include "bls_tower.h"
 
 namespace bls {
@@ -40,11 +41,18 @@ BLS_HD Fq2 fq2_add(const Fq2& a, const Fq2& b) { return Fq2{fq_add(a.c0, b.c0), 
 BLS_HD Fq2 fq2_norm(const Fq2& a) { return Fq2{fq_norm(a.c0), fq_norm(a.c1)}; }
 BLS_HD Fq2 fq2_mul_small(const Fq2& a, uint32_t k) { return Fq2{fq_mul_small(a.c0, k), fq_mul_small(a.c1, k)}; }
 
-// Karatsuba, operands in L form: c0 = t0 - t1 + 64p (< 66p), c1 = t2 - t0 - t1 + 128p (< 130p), both normalised
+// -b1 for fq2_mul: K = 4096p in borrowed digits covering any L-form digit (the chain's operands stay below 2312p)
+constexpr fqb_detail::KConst Q29_KNEG = fqb_detail::k_for(4096, fqb_detail::MASK + 64);
+static_assert(Q29_KNEG.ok && Q29_KNEG.c >= 4096 && Q29_KNEG.c <= 4200, "fq2_mul negation constant");
+// c0 = a0 b0 + a1 (K - b1), c1 = a0 b1 + a1 b0, one reduction each (fq_mul_dot2), operands in L form with
+// b1 < 4096p and a0, a1, b0 < 4096p (a0 b0 + a1 (K - b1) < 4096 (4096 + 4200) p^2 < p R): both coefficients in N form (< 2p).  The Karatsuba form
+// it replaced ran three products, three reductions, two subtractions and two normalisations.
 BLS_HD Fq2 fq2_mul(const Fq2& a, const Fq2& b) {
-  const Fq t0 = fq_mul(a.c0, b.c0), t1 = fq_mul(a.c1, b.c1);
-  const Fq t2 = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
-  return Fq2{fq_norm(fq_subk<Q29_K1>(t0, t1)), fq_norm(fq_subk<Q29_K2>(t2, fq_add(t0, t1)))};
+  FQ_CHECK_SUB(b.c1, Q29_KNEG.d);
+  Fq nb;
+#pragma unroll
+  for (int i = 0; i < 14; i++) nb.d[i] = Q29_KNEG.d[i] - b.c1.d[i];
+  return Fq2{fq_mul_dot2(a.c0, b.c0, a.c1, fq_norm(nb)), fq_mul_dot2(a.c0, b.c1, a.c1, b.c0)};
 }
 // (a0 + a1)(a0 - a1), 2 a0 a1 for a in L form with a1 < 2046p: c0 < 2p, c1 < 4p
 BLS_HD Fq2 fq2_sqr(const Fq2& a) {
@@ -90,7 +98,7 @@ BLS_HD J2Q j2q_add(const J2Q& p, const J2Q& q, bool& exc) {
   FQ_SEQ();
   const Fq2 u1 = fq2_mul(p.x, z2z2);
   FQ_SEQ();
-  const Fq2 u2 = fq2_mul(q.x, z1z1);        // (66, 130)
+  const Fq2 u2 = fq2_mul(q.x, z1z1);        // N form (< 2p)
   FQ_SEQ();
   const Fq2 s1 = fq2_mul(fq2_mul(p.y, q.z), z2z2);
   FQ_SEQ();
@@ -114,7 +122,7 @@ BLS_HD J2Q j2q_add(const J2Q& p, const J2Q& q, bool& exc) {
   FQ_SEQ();
   const Fq2 zz = fq2_norm(fq2_subk<Q29_K2>(fq2_sqr(fq2_norm(fq2_add(p.z, q.z))), fq2_add(z1z1, z2z2)));
   FQ_SEQ();
-  r.z = fq2_mul(zz, h);                                              // (66, 130)
+  r.z = fq2_mul(zz, h);                                              // N form (< 2p)
   FQ_SEQ();
   return r;
 }

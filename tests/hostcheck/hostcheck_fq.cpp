@@ -6,6 +6,7 @@
 #include "bls_ops.h"
 #include "bls_fq_g1.h"
 #include "bls_fq_g2.h"
+#include "bls_fqb.h"
 #include <string.h>
 using namespace bls;
 
@@ -36,6 +37,26 @@ extern "C" void hc_fq_gather(const uint8_t* pts, uint32_t n, uint32_t split, uin
   const Fp zi = fp_inv(Z);
   out_fp(o, fp_mul(X, zi));
   out_fp(o + 48, fp_mul(Y, zi));
+}
+// one-reduction dot product of raw digit vectors: r = (x y + u v) / 2^406, digits (fq_mul_dot2)
+extern "C" void hc_fq_dot2_digits(const uint32_t* x, const uint32_t* y, const uint32_t* u, const uint32_t* v,
+                                  uint32_t* r) {
+  Fq a, b, c, d;
+  memcpy(a.d, x, 56);
+  memcpy(b.d, y, 56);
+  memcpy(c.d, u, 56);
+  memcpy(d.d, v, 56);
+  const Fq o = fq_mul_dot2(a, b, c, d);
+  memcpy(r, o.d, 56);
+}
+// Fp2 products: the untyped chain form (fq2_mul) and the bound-typed one (Fq2B operator*, operands at the
+// Miller accumulation's bounds), both on canonical inputs a, b (96 B each); out = fq2_mul || Fq2B product
+extern "C" void hc_fq2_mul_forms(const uint8_t* a, const uint8_t* b, uint8_t* o) {
+  const Fq2 x = fq2_unpack(in_fp2(a)), y = fq2_unpack(in_fp2(b));
+  out_fp2(o, fq2_pack(fq2_mul(x, y)));
+  const Fq2B<256, 0x20000000ull + 64> xb{{x.c0}, {x.c1}};
+  const Fq2B<4096, 0x20000000ull + 64> yb{{y.c0}, {y.c1}};
+  out_fp2(o + 96, fq2b_pack(xb * yb));
 }
 // one digit-form product of raw digit vectors (14 x u32 each): r = x y / 2^406, digits
 extern "C" void hc_fq_mul_digits(const uint32_t* x, const uint32_t* y, uint32_t* r) {

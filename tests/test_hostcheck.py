@@ -315,6 +315,39 @@ def test_fq_mul_worst_digits():
             assert rv < 2 * O.P and all(d < 2 ** 29 for d in list(r)[:13])
 
 
+def test_fq_dot2_worst_digits():
+    """The one-reduction dot product (fq_mul_dot2, two digit products per column) at the digit bounds the Fp2
+    product feeds it -- operand digits 2^29 + 64 and a negation at 2^30 + 2^29 -- with the column checks compiled
+    in: result congruent to (x y + u v) / 2^406, below 2p, exact 29-bit digits 0..12."""
+    import ctypes
+    f = H.lib().hc_fq_dot2_digits
+    A = ctypes.c_uint32 * 14
+    R = 2 ** 406
+    for dx, dy, du, dv in ((2 ** 29 + 64,) * 4, (2 ** 29 + 64, 2 ** 29 + 64, 2 ** 29 + 64, 3 * 2 ** 29),
+                           (2 ** 29 - 1, 0, 2 ** 29 - 1, 2 ** 29 - 1)):
+        for top in (0, 40, 3000):
+            x, y, u, v = ([d] * 13 + [top] for d in (dx, dy, du, dv))
+            r = A()
+            f(A(*x), A(*y), A(*u), A(*v), r)
+            val = lambda w: sum(d << (29 * i) for i, d in enumerate(w))
+            rv = val(r)
+            assert rv % O.P == (val(x) * val(y) + val(u) * val(v)) * pow(R, -1, O.P) % O.P
+            assert rv < 2 * O.P and all(d < 2 ** 29 for d in list(r)[:13])
+
+
+def test_fq2_mul_forms():
+    """Both digit-form Fp2 products (the chain's fq2_mul and the bound-typed Fq2B product of the Miller
+    accumulation, each a0 b0 + a1 (K - b1), a0 b1 + a1 b0 with one reduction per coefficient) against the
+    oracle's Fp2 product, including zero, one and p - 1 coefficients."""
+    edge = [(0, 0), (1, 0), (0, 1), (O.P - 1, O.P - 1), (O.P - 1, 0)]
+    vals = edge + [rfp2() for _ in range(12)]
+    for a in vals:
+        b = vals[rng.randrange(len(vals))]
+        out = H.call("hc_fq2_mul_forms", H.fp2_b(a), H.fp2_b(b), out=192)
+        want = O.f2_mul(a, b)
+        assert H.b_fp2(out[:96]) == want and H.b_fp2(out[96:]) == want
+
+
 def test_fq_g1_scalar_chain():
     """The r_i apk_i chain of k_sig_lane2 in the digit form (g1q_dbl / g1q_add, checked columns) against the
     oracle for random 64-bit scalars, r = 1 and r = 2^63."""
