@@ -105,6 +105,8 @@ _SIGS = {
     "bls_comm_destroy": (_ip, [_vp]),
     "bls_fav_job_check_comm": (_ip, [_vp, _ip]),
     "bls_comm_abort": (_ip, [_vp]),
+    "bls_host_seed": (_ip, [_vp]),
+    "bls_set_entropy_source": (_ip, [ctypes.c_char_p]),
 }
 
 EXPORTS = tuple(_SIGS)
@@ -122,7 +124,10 @@ def load_library(path: str = LIB_PATH):
         if not os.path.exists(path):
             raise NativeUnavailable(f"{path} not found -- run __graft_entry__.build()")
         lib = ctypes.CDLL(path)
+        ab_build = "BLSMI355X_LIB" in os.environ  # an older library under A/B may lack newer entry points
         for name, (res, args) in _SIGS.items():
+            if ab_build and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -48,6 +48,7 @@ from __future__ import annotations
 import contextlib
 import dis
 import sys
+import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -78,8 +79,9 @@ def _index(code):
 
 
 def _next_ops(code, lasti: int, k: int = 2) -> list[str]:
-    """Opnames of the k instructions after the one at byte offset `lasti` ([] if unknown); TO_BOOL (3.13+,
-    before a conditional jump) is skipped."""
+    """Opnames of the k instructions after the one at byte offset `lasti` ([] if unknown).  TO_BOOL (3.13+,
+    before a conditional jump) is skipped: reserved for a future bytecode port, since callee_name only reads
+    3.10 bytecode and nothing is deferred on other versions (SignatureSets.version_fallback counts those)."""
     ins, pos = _index(code)
     i = pos.get(lasti)
     if i is None:
@@ -198,6 +200,7 @@ class SignatureSets:
         self.ctx = ctx
         self.sets: list[_Set] = []
         self.eager = 0  # verify calls inside deferred() that ran at once (result not asserted)
+        self.version_fallback = 0  # of those, calls run at once only because this interpreter is not 3.10
 
     def try_defer(self, kind: str, args) -> bool:
         """Called by the shim's Verify / FastAggregateVerify / AggregateVerify (bls.py ``_defer``): record the
@@ -206,6 +209,14 @@ class SignatureSets:
         caller = shim_fn.f_back  # only_with_bls's wrapper (named like the shim function), calling it as `fn`
         callee = "fn" if caller is not None and caller.f_code.co_name == shim_fn.f_code.co_name else \
             shim_fn.f_code.co_name
+        if sys.version_info[:2] != (3, 10):  # the bytecode walk reads 3.10 only: batching is lost, say so once
+            self.eager += 1
+            self.version_fallback += 1
+            if self.version_fallback == 1:
+                warnings.warn(f"bls_mi355x.sigsets: deferred() batching needs Python 3.10 bytecode; on "
+                              f"{sys.version_info[0]}.{sys.version_info[1]} every verify call runs at once",
+                              RuntimeWarning, stacklevel=4)
+            return False
         if not result_is_asserted(caller, callee):
             self.eager += 1
             return False

@@ -81,7 +81,8 @@ struct bls_ctx {
   // reservation of (private segment x device wave slots), so they run on two
   // queues instead of on every job's (see k_h2c_fallback).
   hipStream_t fb_stream = nullptr, fe_stream = nullptr;
-  // registry (HBM resident): 96-B RegKey records, validity in x's top bit
+  // registry (HBM resident): RegKey records of 96 B of affine (x, y) padded to 128 B and 128-B aligned (one
+  // cache line per random read), validity in x's top bit; 128 MiB per 2^20 keys, 256 MiB for 2^21
   RegKey* reg = nullptr;
   size_t reg_n = 0;
   size_t reg_cap = 0;  // entries allocated (bls_registry_append grows it)
@@ -89,6 +90,7 @@ struct bls_ctx {
   // multi-GPU exchange of FAV partials (bls_comm_*): one RCCL communicator
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
+  std::string comm_abort_cause;  // why the library aborted the communicator (reported by later calls)
   // per-kernel hipEvent timing of the FAV path (bls_profile_*)
   bool prof_on = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -405,9 +407,12 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
 //   stream2: hash_to_G2(msg) (lane SSWU + wave-program isogeny / cofactor phases)
 //   stream3: signature decode + G2 subgroup check
 //   stream1: KeyValidate of every key (+ their sum)
-// then the two-pair Miller product (k_miller2_vm) and one final-exponentiation
-// check.  Every chain that can be spread over a workgroup is (the h2c and
-// pairing phases); only the square roots and subgroup checks run one lane each.
+// The Miller loop of (-G1, sigma) runs on stream3 right after the signature
+// check, while hash_to_G2 is still running; stream1 then runs only the Miller
+// loop of (apk, H(m)) after the hash, one Fp12 product and one final-
+// exponentiation check.  Every chain that can be spread over a workgroup is
+// (the h2c and pairing phases); only the square roots and subgroup checks run
+// one lane each.
 static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
                           const uint8_t* sig96) {
   Job& J = *ctx->j;
@@ -426,13 +431,13 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_OFFS, 2, d_offs);
   SCR(S_G1A, n, keys);
   SCR(S_OK, n + 2, ok);  // key verdicts | sig verdict | live
-  SCR(S_PC_P, 2, P);
+  SCR(S_PC_P, 3, P);  // P[0] apk, P[1] -G1 (k_percall_pairs); P[2] -G1 for stream3's Miller loop
   SCR(S_G2A, 2, Q);
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
   SCR(S_AV_HCF, h2c_scratch_fd(1), hf);
   SCR(S_AV_FLAG, 1, flag);
-  SCR(S_F, 1, f);
+  SCR(S_F, 3, f);  // f(apk, H) | f(-G1, sigma) | their product
   SCR(S_INT, 4, d_r);
   uint8_t* d_pk = d_in;
   uint8_t* d_sig = d_in + 48 * n;
@@ -450,15 +455,21 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
   HIPCK(hipEventRecord(J.ev_sig, st3));
+  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, P + 2);
+  LK(hipGetLastError());
+  LK(launch_miller_wave(st3, P + 2, Q + 1, ok + n, 1, f + 1));  // a rejected signature gives f = 1; `live` decides
+  HIPCK(hipEventRecord(J.ev_msm, st3));
   LK(launch_key_validate(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
-  LK(launch_miller2(st, P, Q, nullptr, 2, f));  // rejected inputs are identities here; `live` decides
+  LK(launch_miller_wave(st, P, Q, nullptr, 1, f));  // rejected inputs are identities here; `live` decides
+  HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
+  LK(launch_fp12_chunk_prod(st, f, 2, 2, f + 2));
   int live = 0;
   HIPCK(hipMemcpyAsync(&live, ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-  const int fe = run_final_check(ctx, f);  // orders after st
+  const int fe = run_final_check(ctx, f + 2);  // orders after st
   if (fe < 0) return fe;
   HIPCK(hipStreamSynchronize(st));  // `live` is pageable host memory
   return (live && fe) ? 1 : 0;
@@ -969,12 +980,35 @@ static int fav_finish(bls_ctx* ctx, int batch_ok, bool root_bad, uint8_t* d_out)
   return fav_bisect(ctx, root_bad, d_out);
 }
 
-static void host_seed(uint8_t seed[32]) {
-  // RLC scalars must be unpredictable to whoever produced the signatures.
-  FILE* f = fopen("/dev/urandom", "rb");
-  size_t got = f ? fread(seed, 1, 32, f) : 0;
+// Entropy source of the RLC seeds; only bls_set_entropy_source (a test hook) changes it.
+static char g_entropy_path[256] = "/dev/urandom";
+
+int bls_set_entropy_source(const char* path) {
+  if (!path || strlen(path) >= sizeof(g_entropy_path)) return BLS_E_ARG;
+  strcpy(g_entropy_path, path);
+  return 0;
+}
+
+// RLC scalars must be unpredictable to whoever produced the signatures (hard part 6): a short
+// read fails the call closed (BLS_E_DEVICE) instead of continuing with a predictable seed.
+int bls_host_seed(uint8_t* seed32) {
+  if (!seed32) return BLS_E_ARG;
+  FILE* f = fopen(g_entropy_path, "rb");
+  size_t got = f ? fread(seed32, 1, 32, f) : 0;
   if (f) fclose(f);
-  for (size_t i = got; i < 32; i++) seed[i] = (uint8_t)(i * 131 + 7);
+  if (got != 32) {
+    memset(seed32, 0, 32);
+    return BLS_E_DEVICE;
+  }
+  return 0;
+}
+
+static int host_seed(bls_ctx* ctx, uint8_t seed[32]) {
+  if (bls_host_seed(seed) != 0) {
+    ctx->err = "could not read 32 bytes of entropy for the RLC seed";
+    return BLS_E_DEVICE;
+  }
+  return 0;
 }
 
 // One host-buffer FAV batch: copies in, RLC batch check, bisection on failure.
@@ -998,7 +1032,7 @@ static int fav_batch_host(bls_ctx* ctx, const uint32_t* idx, const uint64_t* off
   CK(h2d(ctx, d_m, msgs32, 32 * B));
   CK(h2d(ctx, d_s, sigs96, 96 * B));
   uint8_t seed[32];
-  host_seed(seed);
+  CK(host_seed(ctx, seed));
   Fp12* f;
   CK(fav_prepare(ctx, d_idx, d_offs, B, d_m, d_s, seed, &f));
   int ok = run_final_check(ctx, f);
@@ -1066,7 +1100,7 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
   std::vector<uint64_t> rsc(B);
   {
     uint8_t seed[32];
-    host_seed(seed);
+    CK(host_seed(ctx, seed));
     uint64_t x = 0, y = 0;
     memcpy(&x, seed, 8);
     memcpy(&y, seed + 8, 8);
@@ -1609,6 +1643,7 @@ int bls_comm_init(bls_ctx* ctx, const uint8_t* uid128, int rank, int world) {
   }
   ctx->comm_rank = rank;
   ctx->comm_world = world;
+  ctx->comm_abort_cause.clear();
   return 0;
 }
 
@@ -1666,13 +1701,20 @@ static int job_check_comm(bls_ctx* ctx) {
 int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
   JOB_ENTER(ctx, job);
   if (!ctx->comm) {
-    ctx->err = "bls_comm_init was not called";
+    ctx->err = ctx->comm_abort_cause.empty()
+                   ? "bls_comm_init was not called"
+                   : "the RCCL communicator was aborted after an earlier failure: " + ctx->comm_abort_cause;
     return BLS_E_ARG;
   }
   const int r = job_check_comm(ctx);
-  // an error after the communicator exists leaves the peers waiting in this or a later all-gather: abort it so
-  // their collectives fail instead of hanging (the host sees this rank's negative code)
-  if (r < 0) comm_abort_locked(ctx);
+  // any error here -- a local one included (this rank then skips the all-gather its peers are in) -- leaves
+  // the peers waiting in this or a later all-gather: abort so their collectives fail instead of hanging.  The
+  // first failure's text stays in ctx->err and is repeated by every later call on this context.
+  if (r < 0) {
+    ctx->comm_abort_cause = ctx->err;
+    comm_abort_locked(ctx);
+    ctx->err = "RCCL communicator aborted: " + ctx->comm_abort_cause;
+  }
   return r;
 }
 

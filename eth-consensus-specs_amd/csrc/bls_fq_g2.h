@@ -44,6 +44,10 @@ BLS_HD Fq2 fq2_mul_small(const Fq2& a, uint32_t k) { return Fq2{fq_mul_small(a.c
 // -b1 for fq2_mul: K = 4096p in borrowed digits covering any L-form digit (the chain's operands stay below 2312p)
 constexpr fqb_detail::KConst Q29_KNEG = fqb_detail::k_for(4096, fqb_detail::MASK + 64);
 static_assert(Q29_KNEG.ok && Q29_KNEG.c >= 4096 && Q29_KNEG.c <= 4200, "fq2_mul negation constant");
+// PRECONDITION (every call site; checked only by the BLS_FQ_CHECK host build): both operands in L or N form,
+// i.e. the output of a product or fq_norm -- digits <= 2^29 + 64 and values < 4096p.  An unnormalised fq_add
+// sum (digits up to 2^30) can overflow a 28-product column of fq_mul_dot2 on the device with no error.
+// Chains that need compile-time proofs use the bound-typed Fq2B product of bls_fqb.h instead.
 // c0 = a0 b0 + a1 (K - b1), c1 = a0 b1 + a1 b0, one reduction each (fq_mul_dot2), operands in L form with
 // b1 < 4096p and a0, a1, b0 < 4096p (a0 b0 + a1 (K - b1) < 4096 (4096 + 4200) p^2 < p R): both coefficients in N form (< 2p).  The Karatsuba form
 // it replaced ran three products, three reductions, two subtractions and two normalisations.

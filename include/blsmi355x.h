@@ -266,6 +266,15 @@ int bls_profile_enable(bls_ctx* ctx, int on);  /* also resets the totals */
 int bls_profile_read(bls_ctx* ctx, double* total_ms, uint64_t* counts, int max);
 const char* bls_profile_name(int i);
 
+/* ---- RLC seed entropy (host only, no device needed) ----------------------
+ * bls_host_seed fills 32 bytes from the entropy source (/dev/urandom) and
+ * returns 0, or BLS_E_DEVICE (seed zeroed) when fewer than 32 bytes can be
+ * read: every batch call that draws an RLC seed then fails closed with
+ * BLS_E_DEVICE instead of using a predictable seed.  bls_set_entropy_source
+ * redirects the source (process-wide) and exists for tests. */
+int bls_host_seed(uint8_t* seed32);
+int bls_set_entropy_source(const char* path);
+
 #ifdef __cplusplus
 }
 #endif

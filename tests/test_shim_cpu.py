@@ -125,3 +125,29 @@ def test_scalar_field_arithmetic():
     assert a == 7 and a != b and hash(a) == hash(Scalar(7))
     with pytest.raises(ZeroDivisionError):
         BLSFieldElement(0).inverse()
+
+
+def test_rlc_seed_fails_closed(tmp_path):
+    """a short read of the entropy source must fail the batch call (BLS_E_DEVICE), never
+    continue with a predictable RLC seed (bls_capi.hip bls_host_seed; host only, no device)."""
+    import ctypes
+
+    from bls_mi355x import _native
+    lib = _native.load_library()
+    buf = ctypes.create_string_buffer(32)
+    short = tmp_path / "short"
+    short.write_bytes(b"\x11" * 16)
+    try:
+        for src, want in ((str(tmp_path / "missing"), _native.BLS_E_DEVICE), ("/dev/null", _native.BLS_E_DEVICE),
+                          (str(short), _native.BLS_E_DEVICE)):
+            assert lib.bls_set_entropy_source(src.encode()) == 0
+            assert lib.bls_host_seed(buf) == want, src
+            assert buf.raw == bytes(32)
+        assert lib.bls_set_entropy_source(b"x" * 300) == _native.BLS_E_ARG
+    finally:
+        assert lib.bls_set_entropy_source(b"/dev/urandom") == 0
+    seeds = set()
+    for _ in range(4):
+        assert lib.bls_host_seed(buf) == 0
+        seeds.add(buf.raw)
+    assert len(seeds) == 4

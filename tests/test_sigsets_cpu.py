@@ -143,6 +143,25 @@ def test_deferred_branching_site_gets_the_real_verdict(fakes, monkeypatch):
     assert len(col) == 0 and col.eager == 3 and col.results == []
 
 
+def test_deferred_counts_version_fallback(fakes, monkeypatch):
+    """on an interpreter other than 3.10 nothing can be deferred; the collector must count those
+    calls (version_fallback) and warn once instead of silently losing the batching."""
+    sigsets, _ = fakes
+    from bls_mi355x import bls as shim
+    from bls_mi355x.backend import mi355x_bls
+
+    monkeypatch.setattr(mi355x_bls, "FastAggregateVerify", staticmethod(lambda pks, m, s: True))
+    monkeypatch.setattr(shim.fastest_bls, "FastAggregateVerify", mi355x_bls.FastAggregateVerify)
+    keys = [_pk(i) for i in range(2)]
+    shim.bls_active = True
+    monkeypatch.setattr(sigsets.sys, "version_info", (3, 12, 0, "final", 0))
+    with pytest.warns(RuntimeWarning, match="3.10 bytecode"):
+        with sigsets.deferred(FakeRegistry(keys), check=False) as col:
+            _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
+            _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
+    assert len(col) == 0 and col.eager == 2 and col.version_fallback == 2
+
+
 PATTERNS_SRC = """
 import sys
 from bls_mi355x.sigsets import result_is_asserted
