@@ -24,7 +24,10 @@ runs at any world size through the same RCCL exchange):
                k bad items of every SURVEY §8(d) kind (bisection fallback each
                step), plus AggregateVerify with N = 128 .. 8,192 distinct
                messages as secondary figures.
-The c2 line also carries a C3 epoch-replay figure (`c3`) and, on rank 0, a
+The c2 line also carries the registry-load figure (`registry_load`: bls_registry_load of the 2^20 compressed
+keys the passes then read, keys/s), a C3 epoch-replay figure (`c3`), a C4 figure (`c4`: one 125,000-Verify shard
+per GPU, Verify/s), a C5 figure (`c5`: adversarial 1,024 x 512 batches with 8 bad items, FAV/s, plus
+AggregateVerify N = 128 / 1,024 / 8,192 in pairs/s) and, on rank 0, a
 parity sample (`parity`): an adversarial 1,024 x 512 slice with 8 bad items of
 each kind checked against the construction and, on 16 sampled items, against
 the C oracle; hash_to_G2 of the golden messages against their committed
@@ -358,6 +361,101 @@ def parity_sample(batch, ctx, per_kind: int = 8, oracle_items: int = 16, seed: i
             "known_answers": {"cases": len(ka), "mismatches": int(k_mism)}}
 
 
+# ------------------------------------------------------- secondary configs --
+def run_c4(batch, ctx, timed, total: int, seed: int, rank: int, world: int, steps: int, warmup: int) -> dict:
+    """C4 (BASELINE configs[3], E/utils/bls.py:141-151 call shape): this rank's contiguous shard of `total`
+    single-signature Verify (pk_i = registry[i], distinct messages m_i, sk_i = i + 1) as registry-resident
+    FastAggregateVerify items with n = 1, `steps` pipelined passes; every verdict must be True."""
+    idx, offs, msgs, sks, chunks, (lo, hi) = c4_shard(total, seed, rank, world)
+    rb = batch.ResidentFavBatch(idx, offs, msgs, batch.sign_batch(sks, msgs, ctx=ctx), ctx=ctx, chunks=chunks)
+    dt, oks = timed(rb, steps, warmup)
+    assert all(oks) and rb.verdicts().all(), "a valid C4 Verify was rejected"
+    return {"rb": rb, "dt": dt, "shard_items": hi - lo, "shard": [lo, hi], "chunks": chunks,
+            "verify_s": round(total * steps / dt, 1), "ms_per_shard": round(dt / steps * 1e3, 3), "steps": steps}
+
+
+def run_c5(batch, ctx, timed, n: int, bad: int, seed: int, rank: int, world: int, reg_n: int, steps: int,
+           warmup: int, aggregate_verify: bool) -> dict:
+    """C5 (BASELINE configs[4]): 1,024 x n FastAggregateVerify per rank with `bad` items of the SURVEY.md §8(d)
+    kinds (E/test/altair/bls/test_eth_fast_aggregate_verify.py:38-151 cases; the bisection fallback runs every
+    pass), verdicts against the construction; with aggregate_verify, AggregateVerify with N = 128 / 1,024 / 8,192
+    distinct messages through the drop-in per-call API (E/utils/bls.py:154-164), pairs/s."""
+    B = 1024
+    plan = {int(j): BAD_KINDS[t % len(BAD_KINDS)] for t, j in
+            enumerate(np.random.default_rng(seed + rank).choice(B, size=bad, replace=False))}
+    idx2d, offs, msgs, sigs, expect = adversarial_inputs(batch, ctx, B, n, plan, seed + 17 * rank, reg_n)
+    rb = batch.ResidentFavBatch(idx2d.reshape(-1), offs, b"".join(msgs), bytes(sigs), ctx=ctx)
+    dt, oks = timed(rb, steps, warmup)
+    assert not any(oks) if plan else all(oks)
+    assert (rb.verdicts() == expect).all(), "adversarial verdicts differ from the construction"
+    checks, rounds = batch.fallback_stats(ctx=ctx)
+    out = {"rb": rb, "dt": dt, "items": B, "committee": n, "bad": len(plan), "bad_kinds": sorted(set(plan.values())),
+           "fav_s": round(B * world * steps / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3), "steps": steps,
+           "verdict_mismatches": 0, "fallback_last_step": {"fe_checks": checks, "bisection_rounds": rounds}}
+    if aggregate_verify:  # AggregateVerify with N distinct messages (drop-in per call)
+        from bls_mi355x.backend import mi355x_bls as M
+        av = {}
+        for N in (128, 1024, 8192):
+            ks = [(7919 * (i + 1)) for i in range(N)]
+            pks = batch.sk_to_pk_batch(b"".join(k.to_bytes(32, "big") for k in ks), ctx=ctx)
+            pkl = [pks[48 * i: 48 * i + 48] for i in range(N)]
+            ms = [_msg(b"av", N, i) for i in range(N)]
+            s = batch.sign_batch(b"".join(k.to_bytes(32, "big") for k in ks), b"".join(ms), ctx=ctx)
+            agg = M.Aggregate([s[96 * i: 96 * i + 96] for i in range(N)])
+            assert M.AggregateVerify(pkl, ms, agg)
+            bad_agg = M.Aggregate([s[96 * i: 96 * i + 96] for i in range(N - 1)])  # one signature missing
+            t = time.perf_counter()
+            ok = M.AggregateVerify(pkl, ms, agg)
+            el = time.perf_counter() - t
+            av[str(N)] = {"pairs_s": round(N / el, 1), "ms": round(el * 1e3, 3), "ok": bool(ok),
+                          "rejects_missing_sig": M.AggregateVerify(pkl, ms, bad_agg) is False}
+            assert ok and av[str(N)]["rejects_missing_sig"]
+        out["aggregate_verify"] = av
+    return out
+
+
+def registry_load_figure(ctx, reg_n: int, reps: int = 3) -> dict:
+    """SURVEY.md §8(d) registry load (specs/phase0/beacon-chain.md:787 reads state.validators[*].pubkey; deposits
+    append, :2037-2062): decode + KeyValidate of reg_n compressed keys (pk_i = (i + 1) G1, made on the device)
+    plus the two invalid keys the C5 kinds index and the 8 tests/golden/bls_formats.json key_validate fixtures,
+    through bls_registry_load (host buffer in, validity mask out).  The table it leaves behind is the one the
+    C2 / C3 passes then read, so every later verdict checks the decoded keys.  keys_s = API wall-clock
+    (PCIe-inclusive); kernel_keys_s = keys / k_key_validate's hipEvent time."""
+    import ctypes
+
+    from bls_mi355x import batch
+
+    gen = ctypes.create_string_buffer(48 * reg_n)
+    ctx.check(ctx.lib.bls_registry_generate(ctx.h, 1, reg_n, gen))
+    with open(os.path.join(ROOT, "tests", "golden", "bls_formats.json")) as fh:
+        kv = json.load(fh)["key_validate"]
+    hb = lambda s: bytes.fromhex(s[2:] if s.startswith("0x") else s)  # noqa: E731
+    tail = G1_INF + PK_0x40 + b"".join(hb(c["input"]) for c in kv)
+    data = gen.raw + tail
+    n = len(data) // 48
+    expect = np.concatenate([np.ones(reg_n, np.uint8), np.zeros(2, np.uint8),
+                             np.array([1 if c["output"] else 0 for c in kv], np.uint8)])
+    valid = np.zeros(n, dtype=np.uint8)
+    prof = batch.Profiler(ctx)
+    ts = []
+    for r in range(reps):
+        if r == reps - 1:
+            prof.start()
+        t = time.perf_counter()
+        ctx.check(ctx.lib.bls_registry_load(ctx.h, data, n, valid.ctypes.data))
+        ts.append(time.perf_counter() - t)
+        assert (valid == expect).all(), "registry load: KeyValidate mask differs from the construction / fixtures"
+    kern = prof.read()
+    prof.stop()
+    k_ms = kern["key_validate"][0] / max(kern["key_validate"][1], 1) if kern.get("key_validate") else None
+    best = min(ts)
+    return {"keys": n, "keys_s": round(n / best, 1), "ms": round(best * 1e3, 3),
+            "kernel_ms": round(k_ms, 3) if k_ms else None, "kernel_keys_s": round(n / (k_ms * 1e-3), 1) if k_ms else None,
+            "mask_mismatches": 0, "fixtures": len(kv),
+            "note": "bls_registry_load of 2^20 compressed keys + 2 invalid + 8 bls_formats.json key_validate fixtures; "
+                    "keys_s includes the 48 B/key H2D and the verdict D2H; later C2/C3 passes read this table"}
+
+
 # ---------------------------------------------------------------------- main --
 def _lib_sha() -> str | None:
     try:
@@ -380,6 +478,9 @@ def main():
     ap.add_argument("--c4-total", type=int, default=C4_TOTAL)
     ap.add_argument("--c5-bad", type=int, default=8, help="C5: bad items per batch (kinds cycled)")
     ap.add_argument("--c3-steps", type=int, default=20, help="epochs timed for the c2 line's C3 figure (0: skip)")
+    ap.add_argument("--c4-steps", type=int, default=4, help="125k-Verify shards timed for the c2 line's C4 figure")
+    ap.add_argument("--c5-steps", type=int, default=5, help="adversarial batches timed for the c2 line's C5 figure")
+    ap.add_argument("--no-regload", action="store_true", help="generate the registry instead of loading its keys")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight (no overlap of passes)")
@@ -443,12 +544,16 @@ def main():
 
     # ---- setup (untimed): registry 2^20 (sk_i = i + 1) + two invalid appended keys (C5 kinds) ----
     t_setup = time.perf_counter()
-    reg = batch.Registry(ctx)
-    reg.generate(args.registry, first_sk=1)
-    if args.registry == REG_N:
-        assert reg.append(G1_INF + PK_0x40).tolist() == [0, 0]
-    n = args.committee
     extra = {}
+    reg = batch.Registry(ctx)
+    if args.config == "c2" and args.registry == REG_N and not args.no_regload:
+        # the registry the passes read is decoded from compressed keys (the §8(d) registry-load figure)
+        extra["registry_load"] = registry_load_figure(ctx, REG_N)
+    else:
+        reg.generate(args.registry, first_sk=1)
+        if args.registry == REG_N:
+            assert reg.append(G1_INF + PK_0x40).tolist() == [0, 0]
+    n = args.committee
     rb = None
 
     if args.config == "c2":
@@ -477,47 +582,25 @@ def main():
         ops_step = item_ops(C3_N) * units + BATCH_OPS * world
         extra["ms_per_epoch"] = round(dt / args.steps * 1e3, 3)
     elif args.config == "c4":
-        idx, offs, msgs, sks, chunks, (lo, hi) = c4_shard(args.c4_total, args.seed, rank, world)
-        B = hi - lo
-        rb = batch.ResidentFavBatch(idx, offs, msgs, batch.sign_batch(sks, msgs, ctx=ctx), ctx=ctx, chunks=chunks)
+        r4 = run_c4(batch, ctx, timed, args.c4_total, args.seed, rank, world, args.steps, args.warmup)
+        rb, dt, B, chunks = r4.pop("rb"), r4.pop("dt"), r4["shard_items"], r4["chunks"]
         setup_s = time.perf_counter() - t_setup
-        dt, oks = timed(rb, args.steps, args.warmup)
-        assert all(oks) and rb.verdicts().all()
         units, unit, scaling = args.c4_total, "Verify/s", "strong"
         workload = (f"C4 gossip firehose: {args.c4_total} single-signature Verify (pk_i = registry[i], distinct "
                     f"messages), contiguous shards of {B} per GPU in {chunks} job(s)")
         ops_step = item_ops(1) * units + BATCH_OPS * chunks * world
     else:  # c5
-        B = 1024
-        plan = {int(j): BAD_KINDS[t % len(BAD_KINDS)] for t, j in
-                enumerate(np.random.default_rng(args.seed + rank).choice(B, size=args.c5_bad, replace=False))}
-        idx2d, offs, msgs, sigs, expect = adversarial_inputs(batch, ctx, B, n, plan, args.seed + 17 * rank,
-                                                             args.registry)
-        rb = batch.ResidentFavBatch(idx2d.reshape(-1), offs, b"".join(msgs), bytes(sigs), ctx=ctx)
+        r5 = run_c5(batch, ctx, timed, n, args.c5_bad, args.seed, rank, world, args.registry, args.steps, args.warmup,
+                    aggregate_verify=rank == 0)
+        rb, dt, B = r5.pop("rb"), r5.pop("dt"), r5["items"]
         setup_s = time.perf_counter() - t_setup
-        dt, oks = timed(rb, args.steps, args.warmup)
-        assert (rb.verdicts() == expect).all(), "adversarial verdicts differ from the construction"
-        checks, rounds = batch.fallback_stats(ctx=ctx)
         units, unit, scaling = B * world, "FAV/s", "weak"
         workload = (f"C5 adversarial FAV batches: {B} x {n} per GPU with {args.c5_bad} bad items "
-                    f"({', '.join(sorted(set(plan.values())))}), bisection fallback every step")
+                    f"({', '.join(r5['bad_kinds'])}), bisection fallback every step")
         ops_step = item_ops(n) * units + BATCH_OPS * world
-        extra["fallback_last_step"] = {"fe_checks": checks, "bisection_rounds": rounds}
-        if rank == 0:  # AggregateVerify with N distinct messages (drop-in per call, replicas per rank)
-            from bls_mi355x.backend import mi355x_bls as M
-            av = {}
-            for N in (128, 1024, 8192):
-                ks = [(7919 * (i + 1)) for i in range(N)]
-                pks = batch.sk_to_pk_batch(b"".join(k.to_bytes(32, "big") for k in ks), ctx=ctx)
-                pkl = [pks[48 * i: 48 * i + 48] for i in range(N)]
-                ms = [_msg(b"av", N, i) for i in range(N)]
-                s = batch.sign_batch(b"".join(k.to_bytes(32, "big") for k in ks), b"".join(ms), ctx=ctx)
-                agg = M.Aggregate([s[96 * i: 96 * i + 96] for i in range(N)])
-                assert M.AggregateVerify(pkl, ms, agg)
-                t = time.perf_counter()
-                ok = M.AggregateVerify(pkl, ms, agg)
-                av[str(N)] = {"pairs_s": round(N / (time.perf_counter() - t), 1), "ok": bool(ok)}
-            extra["aggregate_verify"] = av
+        extra["fallback_last_step"] = r5["fallback_last_step"]
+        if "aggregate_verify" in r5:
+            extra["aggregate_verify"] = r5["aggregate_verify"]
 
     ms_step = dt / args.steps * 1e3
     value = units * args.steps / dt
@@ -534,6 +617,22 @@ def main():
                        "workload": f"{C3_SLOTS} slots x {C3_PER_SLOT} committees of {C3_N} (2^20 registry), "
                                    f"one RLC verdict per epoch, epochs pipelined like C2"}
         rb3.free()
+    # ---- C4 / C5 figures beside the C2 headline (BASELINE configs[3], configs[4]; their own --config runs scale
+    # them to any world size) ----
+    if args.config == "c2" and args.registry == REG_N:
+        if args.c4_steps > 0:  # one 125,000-Verify shard per GPU (the 8-GPU shard of 10^6)
+            r4 = run_c4(batch, ctx, timed, C4_CHUNK * world, args.seed, rank, world, args.c4_steps, 1)
+            r4.pop("rb").free()
+            r4.pop("dt")
+            r4["workload"] = f"{C4_CHUNK} single-signature Verify per GPU (pk_i = registry[i], distinct messages)"
+            extra["c4"] = r4
+        if args.c5_steps > 0:
+            r5 = run_c5(batch, ctx, timed, n, args.c5_bad, args.seed, rank, world, args.registry, args.c5_steps, 1,
+                        aggregate_verify=rank == 0)
+            r5.pop("rb").free()
+            r5.pop("dt")
+            r5["workload"] = f"1024 x {n} FAV per GPU with {args.c5_bad} bad items, bisection fallback every pass"
+            extra["c5"] = r5
 
     # per-kernel execution times: one batch at a time, hipEvents around each launch (after the timed region)
     kern = {}

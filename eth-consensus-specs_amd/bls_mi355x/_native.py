@@ -107,6 +107,8 @@ _SIGS = {
     "bls_comm_abort": (_ip, [_vp]),
     "bls_host_seed": (_ip, [_vp]),
     "bls_set_entropy_source": (_ip, [ctypes.c_char_p]),
+    "bls_test_force_h2c_fallback": (_ip, [_vp, _u8p, _sz]),
+    "bls_test_hash_to_g2_batch": (_ip, [_vp, _u8p, _sz, _vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -87,6 +87,10 @@ struct bls_ctx {
   size_t reg_n = 0;
   size_t reg_cap = 0;  // entries allocated (bls_registry_append grows it)
   uint64_t reg_gen = 0;  // bumped whenever the table is replaced (load / generate)
+  // test hook (bls_test_force_h2c_fallback): items whose hash_to_G2 is routed to k_h2c_fallback regardless of
+  // the lane kernels' flags; null in every product use
+  int* force_fb = nullptr;
+  size_t force_fb_n = 0;
   // multi-GPU exchange of FAV partials (bls_comm_*): one RCCL communicator
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
@@ -101,7 +105,7 @@ struct bls_ctx {
 
 static const char* const PROF_NAMES[] = {"fav_gather", "sig_decode", "fav_hash", "g2_sum",        "sig_pair", "miller",
                                          "fp12_prod",  "final_exp",  "fav_finish", "partials_prod", "sig_vm",
-                                         "msm",        "miller_lines"};
+                                         "msm",        "miller_lines", "key_validate"};
 static const int PROF_N = sizeof(PROF_NAMES) / sizeof(PROF_NAMES[0]);
 
 namespace {
@@ -267,9 +271,18 @@ int run_final_checks_sel(bls_ctx* ctx, const Fp12* f, const uint32_t* sel, size_
 
 // hash_to_G2 exceptional items (k_h2c_fallback) on the context's fallback
 // stream, between the h2c phases on `st` and whatever `st` runs next.
-int h2c_fallback(bls_ctx* ctx, hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, const int* flag,
+__global__ void k_or_flags(size_t B, const int* force, int* flag) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B && force[i]) flag[i] = 1;
+}
+
+int h2c_fallback(bls_ctx* ctx, hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, int* flag,
                  G2A* H) {
   Job& J = *ctx->j;
+  if (ctx->force_fb && B && B <= ctx->force_fb_n) {  // test hook only
+    hipLaunchKernelGGL(k_or_flags, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, B, ctx->force_fb, flag);
+    LK(hipGetLastError());
+  }
   HIPCK(hipEventRecord(J.ev_h2c, st));
   HIPCK(hipStreamWaitEvent(ctx->fb_stream, J.ev_h2c, 0));
   LK(launch_h2c_fallback(ctx->fb_stream, B, msgs, offs, flag, H));
@@ -386,6 +399,7 @@ void bls_ctx_destroy(bls_ctx* ctx) {
     (void)hipEventDestroy(p.second);
   }
   if (ctx->reg) (void)hipFree(ctx->reg);
+  if (ctx->force_fb) (void)hipFree(ctx->force_fb);
   delete ctx;
 }
 
@@ -687,6 +701,57 @@ int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8
   return 1;
 }
 
+// ------------------------------------------------------------ test hooks --
+// Route the items i < n with mask[i] != 0 of every later hash_to_G2 through k_h2c_fallback (the reference-path
+// formulas) as if the lane kernels had flagged them; n = 0 clears.  The lane kernels flag only g(x1) = 0, g(x) in
+// Fp, a vanishing isogeny denominator or an exceptional chain addition, none of which hash outputs reach in
+// practice, so without this the routing and the fallback's overwrite of H[i] would go untested on the device.
+int bls_test_force_h2c_fallback(bls_ctx* ctx, const uint8_t* mask, size_t n) {
+  API_ENTER(ctx);
+  if (!mask && n) return BLS_E_ARG;
+  HIPCK(hipDeviceSynchronize());
+  if (ctx->force_fb) HIPCK(hipFree(ctx->force_fb));
+  ctx->force_fb = nullptr;
+  ctx->force_fb_n = 0;
+  if (!n) return 0;
+  std::vector<int> m(n);
+  for (size_t i = 0; i < n; i++) m[i] = mask[i] ? 1 : 0;
+  HIPCK(hipMalloc(&ctx->force_fb, n * sizeof(int)));
+  HIPCK(hipMemcpy(ctx->force_fb, m.data(), n * sizeof(int), hipMemcpyHostToDevice));
+  ctx->force_fb_n = n;
+  return 0;
+}
+
+__global__ void k_g2_compress_many(size_t n, const G2A* in, uint8_t* out96) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) g2_compress(out96 + 96 * i, in[i]);
+}
+
+// hash_to_G2 of n 32-byte messages (DST POP) through the FAV batch's lane kernels and fallback routing
+// (launch_h2c + h2c_fallback, exactly as bls_fav_* run them), compressed: out96[96 i ..] = H(m_i).
+int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96) {
+  API_ENTER(ctx);
+  if ((!msgs32 || !out96) && n) return BLS_E_ARG;
+  if (!n) return 0;
+  uint8_t *d_m, *d_out;
+  Fd* hf;
+  G2A* H;
+  int* flag;
+  SCR(S_IN0, 32 * n, d_m);
+  SCR(S_IN2, 96 * n, d_out);
+  SCR(S_AV_HCF, h2c_scratch_fd(n), hf);
+  SCR(S_AV_FLAG, n, flag);
+  SCR(S_G2A, n, H);
+  hipStream_t st = ctx->j->stream;
+  CK(h2d(ctx, d_m, msgs32, 32 * n));
+  LK(launch_h2c(st, n, d_m, nullptr, hf, H, flag));
+  CK(h2c_fallback(ctx, st, n, d_m, nullptr, flag, H));
+  hipLaunchKernelGGL(k_g2_compress_many, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, H, d_out);
+  LK(hipGetLastError());
+  CK(d2h(ctx, out96, d_out, 96 * n));
+  return 0;
+}
+
 // ------------------------------------------------------------- registry --
 // Decode + KeyValidate n keys into reg[first ..] (valid[] = the verdicts).
 static int registry_fill(bls_ctx* ctx, const uint8_t* pks48, size_t n, size_t first, uint8_t* out_valid) {
@@ -698,7 +763,7 @@ static int registry_fill(bls_ctx* ctx, const uint8_t* pks48, size_t n, size_t fi
   SCR(S_OK, n, d_ok);
   SCR(S_IN3, n, d_valid);
   CK(h2d(ctx, d_in, pks48, 48 * n));
-  LK(launch_key_validate(ctx->j->stream, d_in, n, d_a, d_ok));
+  PROF(13, launch_key_validate(ctx->j->stream, d_in, n, d_a, d_ok));
   LK(launch_reg_pack(ctx->j->stream, d_a, d_ok, n, ctx->reg + first, d_valid));
   if (out_valid) CK(d2h(ctx, out_valid, d_valid, n));
   HIPCK(hipStreamSynchronize(ctx->j->stream));

@@ -16,12 +16,60 @@ __device__ static const uint8_t DST_POP_DEV[43] = {
 static __device__ __forceinline__ size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
 // ---------------------------------------------------------------- decode --
+// [|x|] P by the complete projective formulas in the digit form (bls_fq_g1.h: g1q_dbl / g1q_add, the chain of
+// k_sig_lane2); the base is affine (x, y) when AFF, else the projective point b.
+template <bool AFF>
+static __device__ __forceinline__ G1Q g1q_mul_xabs(const G1Q& b) {
+  G1Q m = b;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    m = g1q_dbl(m);
+    if ((X_ABS >> i) & 1ull) m = AFF ? g1q_add_aff(m, b.x, b.y) : g1q_add(m, b);
+  }
+  return m;
+}
+
+// KeyValidate (E/utils/bls.py:395-397; py_ecc pubkey_to_G1 decode rules, identity rejected, subgroup check) of one
+// 48-byte key, every product in the redundant digit form of bls_fq.h and inlined (the packed form's out-of-line
+// square root and Jacobian chains cost this kernel a 1,552-B private segment):
+//   decode: flags, x < p, y = (x^3 + 4)^((p+1)/4) (fq_pow_w3), y^2 == x^3 + 4, the sign bit picks y or -y;
+//   subgroup (bls_curve.h g1_in_subgroup): phi(P) == -[x^2] P with phi(x, y) = (beta x, y), i.e. for
+//   [|x|]([|x|] P) = (X : Y : Z):  beta x Z == X  and  y Z + Y == 0  (Z == 0, the identity, fails the second).
 __global__ void __launch_bounds__(64) k_key_validate(const uint8_t* pks48, size_t n, G1A* out, int* ok) {
-  size_t i = gtid();
+  const size_t i = gtid();
   if (i >= n) return;
-  G1A a;
-  int v = key_validate(a, pks48 + 48 * i);
-  if (!v) a = G1A{fp_zero(), fp_zero(), true};
+  // 48 big-endian bytes; records are 48 B apart, so word loads stay 4-byte aligned
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(pks48 + 48 * i);
+  Fp x;
+#pragma unroll
+  for (int k = 0; k < 12; k++) x.l[11 - k] = __builtin_bswap32(w[k]);
+  const uint32_t flags = x.l[11] >> 24;
+  const bool c_flag = flags & 0x80, b_flag = flags & 0x40, a_flag = flags & 0x20;
+  x.l[11] &= 0x1fffffffu;
+  G1A a{fp_zero(), fp_zero(), true};
+  int v = 0;
+  // the identity (b_flag) and every malformed encoding fail KeyValidate
+  if (c_flag && !b_flag && !fp_is_zero(x) && raw_lt_p(x)) {
+    const Fq xm = fq_mul(fq_unpack(x), fq_unpack(FP_R2));  // Montgomery form, N
+    const Fq rhs = fq_add(fq_mul(fq_sqr(xm), xm), fq_unpack(FP_B1));
+    Fq y = fq_pow_w3(rhs, EXP_SQRT, EXP_SQRT_BITS);
+    if (fp_eq(fq_pack(fq_sqr(y)), fq_pack(rhs))) {
+      Fp yc = fq_pack_n(y);
+      Fq one = fq_zero();
+      one.d[0] = 1;
+      if (raw_gt_half(fq_pack_n(fq_mul(y, one))) != a_flag) yc = fp_neg(yc);
+      const Fp xc = fq_pack_n(xm);
+      y = fq_unpack(yc);
+      const G1Q P{xm, y, fq_unpack(FP_ONE)};
+      const G1Q Q = g1q_mul_xabs<false>(g1q_mul_xabs<true>(P));
+      const bool eq_x = fp_eq(fq_pack(fq_mul(fq_mul(xm, fq_unpack(FP_BETA)), Q.z)), fq_pack(Q.x));
+      const bool eq_y = fp_is_zero(fq_pack(fq_add(fq_mul(y, Q.z), Q.y)));
+      if (eq_x && eq_y) {
+        a = G1A{xc, yc, false};
+        v = 1;
+      }
+    }
+  }
   out[i] = a;
   ok[i] = v;
 }

@@ -275,6 +275,15 @@ const char* bls_profile_name(int i);
 int bls_host_seed(uint8_t* seed32);
 int bls_set_entropy_source(const char* path);
 
+/* ---- test hooks (tests/ only; no reference counterpart) -------------------
+ * bls_test_force_h2c_fallback: items i < n with mask[i] != 0 of every later
+ * hash_to_G2 (batch, per-call, AggregateVerify) take the reference-path
+ * fallback kernel as if the lane kernels had flagged them; n = 0 clears.
+ * bls_test_hash_to_g2_batch: hash_to_G2 (DST POP) of n 32-byte messages through
+ * the FAV batch's kernels and fallback routing, compressed into out96. */
+int bls_test_force_h2c_fallback(bls_ctx* ctx, const uint8_t* mask, size_t n);
+int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96);
+
 #ifdef __cplusplus
 }
 #endif

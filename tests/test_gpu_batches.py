@@ -216,3 +216,80 @@ def test_fav_batch_signatures_outside_g2(batch, registry):
         sig = bytes(sigs[96 * j: 96 * j + 96])
         assert OC.FastAggregateVerify(pks, msgs[j], sig) is expect[j]
         assert shim.FastAggregateVerify(pks, msgs[j], sig) is expect[j]
+
+
+def test_h2c_fallback_routing_forced(batch, registry):
+    """items of a batch forced onto k_h2c_fallback (bls_test_force_h2c_fallback, as if the
+    lane SSWU had returned `rare` or a chain addition had been exceptional) get the reference-path H(m), which
+    overwrites the lane kernels' output: the points equal the C oracle's hash_to_G2, and FAV / per-call Verify /
+    AggregateVerify verdicts through the same routing match the construction."""
+    import ctypes
+
+    from bls_mi355x import _native
+    from bls_mi355x.backend import mi355x_bls as M
+
+    ctx = _native.context()
+    n = 70  # past one 64-lane workgroup of the fallback's stride loop
+    msgs = [hashlib.sha256(b"forced-fallback" + j.to_bytes(4, "little")).digest() for j in range(n)]
+    forced = {0, 5, 63, 64, 69}
+    mask = bytes(1 if j in forced else 0 for j in range(n))
+    ctx.check(ctx.lib.bls_test_force_h2c_fallback(ctx.h, mask, n))
+    try:
+        out = ctypes.create_string_buffer(96 * n)
+        ctx.check(ctx.lib.bls_test_hash_to_g2_batch(ctx.h, b"".join(msgs), n, out))
+        for j in sorted(forced) + [1, 2, 62, 65]:
+            assert out.raw[96 * j: 96 * j + 96] == OC.hash_to_g2(msgs[j]), j
+        # a FAV batch whose forced items include valid and invalid ones
+        B, k = n, 16
+        idx, offs, bmsgs, sigs = _make_batch(batch, B, k, seed=0xFB)
+        bad = {5: "wrong_msg", 64: "wrong_msg", 7: "wrong_msg"}
+        for j, kind in bad.items():
+            _corrupt(sigs, bmsgs, j, kind, B)
+        got = batch.fast_aggregate_verify_batch(idx, offs, b"".join(bmsgs), bytes(sigs))
+        expect = np.array([j not in bad for j in range(B)])
+        assert (got == expect).all(), np.nonzero(got != expect)
+        # per-call Verify and AggregateVerify (n = 1 and 3 messages) through the same routing
+        pk, m = OC.SkToPk(11), msgs[0]
+        assert M.Verify(pk, m, OC.Sign(11, m)) is True
+        assert M.Verify(pk, m, OC.Sign(12, m)) is False
+        pks = [OC.SkToPk(k) for k in (21, 22, 23)]
+        agg = OC.Aggregate([OC.Sign(k, msgs[i]) for i, k in enumerate((21, 22, 23))])
+        assert M.AggregateVerify(pks, msgs[:3], agg) is True
+        assert M.AggregateVerify(pks, [msgs[0], msgs[2], msgs[1]], agg) is False
+    finally:
+        ctx.check(ctx.lib.bls_test_force_h2c_fallback(ctx.h, None, 0))
+    # cleared: the lane path again, same points
+    out2 = ctypes.create_string_buffer(96 * n)
+    ctx.check(ctx.lib.bls_test_hash_to_g2_batch(ctx.h, b"".join(msgs), n, out2))
+    assert out2.raw == out.raw
+
+
+def test_resident_batch_chunked(batch, registry):
+    """a ResidentFavBatch split into chunks (one FAV job per chunk, the C4 firehose's shape) with fewer
+    jobs in flight than chunks: bad items in several chunks including the last item of the last chunk; every
+    pass fails its batch check, and the stitched verdicts equal the unchunked batch's and the construction."""
+    B, k, chunks = 512, 8, 4
+    idx, offs, msgs, sigs = _make_batch(batch, B, k, seed=0xC4)
+    bad = {3: "wrong_msg", 130: "inf_sig", 300: "zero_sig", B - 1: "wrong_msg"}
+    for j, kind in bad.items():
+        _corrupt(sigs, msgs, j, kind, B)
+    expect = np.array([j not in bad for j in range(B)])
+    rbc = batch.ResidentFavBatch(idx, offs, b"".join(msgs), bytes(sigs), chunks=chunks)
+    rb1 = batch.ResidentFavBatch(idx, offs, b"".join(msgs), bytes(sigs))
+    try:
+        oks = rbc.run_pipelined([bytes([s]) * 32 for s in range(3)], depth=2)
+        assert oks == [False] * 3
+        vc = rbc.verdicts()
+        assert rb1.run_pipelined([b"\x07" * 32], depth=1) == [False]
+        assert (vc == rb1.verdicts()).all() and (vc == expect).all(), np.nonzero(vc != expect)
+        # a clean chunked batch passes every pass
+        idx2, offs2, msgs2, sigs2 = _make_batch(batch, B, k, seed=0xC5)
+        rb2 = batch.ResidentFavBatch(idx2, offs2, b"".join(msgs2), bytes(sigs2), chunks=chunks)
+        try:
+            assert rb2.run_pipelined([b"\x01" * 32, b"\x02" * 32], depth=3) == [True, True]
+            assert rb2.verdicts().all()
+        finally:
+            rb2.free()
+    finally:
+        rbc.free()
+        rb1.free()

@@ -421,3 +421,47 @@ def test_fp_inv_safegcd():
     for v in vals:
         out = H.call("hc_fp_inv_sg", H.fp_b(v), out=48)
         assert int.from_bytes(out, "big") == (pow(v, -1, O.P) if v else 0), hex(v)
+
+
+def _sswu_preimage_gx_in_fp(seed: int):
+    """A u whose simplified-SWU image x = x1 has g(x1) in Fp (so g(x1) is a square in Fp2, x = x1 is taken, and
+    y = sqrt(g(x1)) needs the a1 = 0 branch): pick x1 = a + b i with Im(x1^3 + A x1 + B) = 3 a^2 b - b^3 + 240 a +
+    1012 = 0 (A = 240 i, B = 1012 (1 + i)), then invert x1 = (-B/A)(1 + 1/(t^2 + t)), t = Z u^2."""
+    rnd = random.Random(seed)
+    P = O.P
+    while True:
+        b = rnd.randrange(1, P)
+        disc = (240 * 240 - 12 * b * (1012 - b ** 3)) % P
+        if not O.fp_is_square(disc):
+            continue
+        a = (-240 + O.fp_sqrt(disc)) * pow(6 * b, -1, P) % P
+        x1 = (a, b)
+        gx = O.f2_add(O.f2_add(O.f2_mul(O.f2_sqr(x1), x1), O.f2_mul(O.SSWU_A, x1)), O.SSWU_B)
+        assert gx[1] == 0
+        c = O.f2_sub(O.f2_mul(x1, O.f2_mul(O.f2_neg(O.SSWU_A), O.f2_inv(O.SSWU_B))), O.F2_ONE)  # 1 / (t^2 + t)
+        if O.f2_is_zero(c):
+            continue
+        d = O.f2_add(O.F2_ONE, O.f2_muls(O.f2_inv(c), 4))  # t = (-1 +- sqrt(1 + 4 / c)) / 2
+        if not O.f2_is_square(d):
+            continue
+        t = O.f2_mul(O.f2_add(O.f2_neg(O.F2_ONE), O.f2_sqrt(d)), O.f2_inv(O.f2(2)))
+        u2 = O.f2_mul(t, O.f2_inv(O.SSWU_Z))
+        if not O.f2_is_square(u2):
+            continue
+        u = O.f2_sqrt(u2)
+        if O.map_to_curve_sswu(u)[0] == x1:
+            return u
+
+
+def test_sswu_rare_case_flagged():
+    """VERDICT r3 item 6 (host side): an input whose g(x) lies in Fp makes the inline SSWU of the FAV h2c kernel
+    return rare = 1 (its item goes to k_h2c_fallback), and the reference-path SSWU of the fallback maps it to the
+    oracle's point."""
+    for seed in (1, 2):
+        u = _sswu_preimage_gx_in_fp(seed)
+        rare, _ = H.call("hc_map_to_curve_lane_i", H.fp2_b(u), out=192, ret=True)
+        assert rare == 1
+        out = H.call("hc_map_to_curve", H.fp2_b(u), out=192)
+        assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
+        out = H.call("hc_map_to_curve_lane", H.fp2_b(u), out=192)
+        assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
