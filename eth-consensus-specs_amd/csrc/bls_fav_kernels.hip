@@ -7,6 +7,8 @@
 //   k_sig_decode      signature decompression + RLC scalar, one lane per item
 //   k_g1_affine_b     r_i apk_i to affine (after k_sig_lane2, bls_chain_lane.hip)
 //   k_h2c_fallback    the reference-path hash_to_G2 for flagged items
+#include <utility>
+
 #include "bls_kernels.h"
 #include "bls_lane.h"
 #include "bls_fq_g2.h"
@@ -47,19 +49,38 @@ __global__ void __launch_bounds__(64) k_h2c_fallback_var(size_t B, const uint8_t
 }
 
 // ----------------------------------------------------------- signatures --
-// RLC scalar r_i = first 8 bytes of SHA-256(seed || i || msg || sig), nonzero.
+// RLC scalar r_i = first 8 bytes of SHA-256(seed || i (8 bytes LE) || msg || sig), nonzero.  The 168-byte input
+// is three blocks whose word positions are all fixed, so the message words are loaded straight into the
+// schedule registers (bls_xmd32.h sha256_compress_w, constant indices): the byte-streaming Sha256 state of
+// bls_sha256.h kept its block buffer in a private segment.
+static __device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) {
+  return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(p));
+}
 static __device__ uint64_t rlc_scalar_fav(const uint8_t* seed32, uint64_t i, const uint8_t* msg32,
                                           const uint8_t* sig96) {
-  Sha256 sh;
-  sha256_init(sh);
-  sha256_update(sh, seed32, 32);
-  for (int k = 0; k < 8; k++) sha256_byte(sh, (uint8_t)(i >> (8 * k)));
-  sha256_update(sh, msg32, 32);
-  sha256_update(sh, sig96, 96);
-  uint8_t d[32];
-  sha256_final(sh, d);
-  uint64_t r = 0;
-  for (int k = 0; k < 8; k++) r = (r << 8) | d[k];
+  uint32_t st[8], blk[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) st[k] = SHA256_IV[k];
+#pragma unroll
+  for (int k = 0; k < 8; k++) blk[k] = ld_be32(seed32 + 4 * k);
+  blk[8] = __builtin_bswap32((uint32_t)i);
+  blk[9] = __builtin_bswap32((uint32_t)(i >> 32));
+#pragma unroll
+  for (int k = 0; k < 6; k++) blk[10 + k] = ld_be32(msg32 + 4 * k);
+  sha256_compress_w(st, blk);
+  blk[0] = ld_be32(msg32 + 24);
+  blk[1] = ld_be32(msg32 + 28);
+#pragma unroll
+  for (int k = 0; k < 14; k++) blk[2 + k] = ld_be32(sig96 + 4 * k);
+  sha256_compress_w(st, blk);
+#pragma unroll
+  for (int k = 0; k < 10; k++) blk[k] = ld_be32(sig96 + 56 + 4 * k);
+  blk[10] = 0x80000000u;
+#pragma unroll
+  for (int k = 11; k < 15; k++) blk[k] = 0;
+  blk[15] = 168 * 8;
+  sha256_compress_w(st, blk);
+  const uint64_t r = ((uint64_t)st[0] << 32) | st[1];
   return r ? r : 1;
 }
 
@@ -71,9 +92,11 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
                                                    const uint8_t* seed32, G2A* sig, uint64_t* rsc, int* dstat) {
   const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= B) return;
+  // the hash first: nothing of the decompression is live across its three compressions
+  const uint64_t r = rlc_scalar_fav(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i);
   G2A q{fp2_zero(), fp2_zero(), true};
-  const int st = g2_decompress_lane(q, sigs96 + 96 * i) == DEC_OK ? 1 : 0;
-  rsc[i] = st ? rlc_scalar_fav(seed32, i, msgs32 + 32 * i, sigs96 + 96 * i) : 0;
+  const int st = g2_decompress_lane_w(q, sigs96 + 96 * i) == DEC_OK ? 1 : 0;
+  rsc[i] = st ? r : 0;
   sig[i] = q;
   dstat[i] = st;
 }
@@ -87,6 +110,16 @@ __global__ void __launch_bounds__(64) k_sig_decode(size_t B, const uint8_t* msgs
 // inversions' SIMD time.  A zero denominator (identity, or a skipped item)
 // enters the products as 1 and gets the same output as the one-item kernels.
 constexpr int AFF_K = 8;
+
+// f(integral_constant<k>) for k = AFF_K - 1 .. 0: the walk-back loops of the affine kernels with compile-time k
+// (as `#pragma unroll` loops the compiler left them rolled, pre[] indexed at run time in a private segment)
+template <class F, int... K>
+__device__ __forceinline__ void aff_walk_back(F&& f, std::integer_sequence<int, K...>) {
+  (f(std::integral_constant<int, (int)sizeof...(K) - 1 - K>{}), ...);
+}
+// k_h2c_affine_b converts 4 items per lane: its Fp2 products beside 8 prefix products pushed it past the register
+// file (112 B/lane of private memory); the extra inversion per 4 items is ~5 FME against ~40 for the conversions
+constexpr int AFF_K2 = 4;
 
 __global__ void __launch_bounds__(64) k_g1_affine_b(size_t B, const int* status, const G1P* rPj, G1A* rP) {
   const size_t base = (size_t)blockIdx.x * 64 * AFF_K + threadIdx.x;
@@ -103,31 +136,31 @@ __global__ void __launch_bounds__(64) k_g1_affine_b(size_t B, const int* status,
     pre[k] = acc;
   }
   Fp inv = fp_inv_sg_i(acc);  // 1 / (z_0 ... z_{K-1})
-#pragma unroll
-  for (int k = AFF_K - 1; k >= 0; --k) {
+  aff_walk_back([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     const size_t i = base + 64 * k;
-    if (i >= B) continue;
-    const bool live = status[i] != 0;
+    const bool in = i < B;
+    const bool live = in && status[i] != 0;
     const Fp zk = live ? rPj[i].z : FP_ONE;
-    const Fp zi = k ? fp_mul_i(inv, pre[k - 1]) : inv;
-    if (k && !zero[k]) inv = fp_mul_i(inv, zk);
+    const Fp zi = k ? fp_mul_i(inv, pre[k ? k - 1 : 0]) : inv;
+    if (in && k && !zero[k]) inv = fp_mul_i(inv, zk);
     G1A o{fp_zero(), fp_zero(), true};
     if (live) {
       const G1P q = rPj[i];
       const Fp zz = zero[k] ? fp_zero() : zi;  // fp_inv(0) = 0, as k_g1_affine
       o = G1A{fp_mul_i(q.x, zz), fp_mul_i(q.y, zz), false};
     }
-    rP[i] = o;
-  }
+    if (in) rP[i] = o;
+  }, std::make_integer_sequence<int, AFF_K>{});
 }
 
 __global__ void __launch_bounds__(64) k_h2c_affine_b(size_t B, const int* status, const Fd* hf, G2A* H) {
-  const size_t base = (size_t)blockIdx.x * 64 * AFF_K + threadIdx.x;
-  Fp pre[AFF_K];
-  bool zero[AFF_K];
+  const size_t base = (size_t)blockIdx.x * 64 * AFF_K2 + threadIdx.x;
+  Fp pre[AFF_K2];
+  bool zero[AFF_K2];
   Fp acc = FP_ONE;
 #pragma unroll
-  for (int k = 0; k < AFF_K; ++k) {
+  for (int k = 0; k < AFF_K2; ++k) {
     const size_t i = base + 64 * k;
     Fp n = FP_ONE;
     if (i < B && (!status || status[i])) {
@@ -141,22 +174,22 @@ __global__ void __launch_bounds__(64) k_h2c_affine_b(size_t B, const int* status
     pre[k] = acc;
   }
   Fp inv = fp_inv_sg_i(acc);
-#pragma unroll
-  for (int k = AFF_K - 1; k >= 0; --k) {
+  aff_walk_back([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     const size_t i = base + 64 * k;
-    if (i >= B) continue;
-    const Fd* r = hf + HCF * i + HCF_A;
-    const Fp2 Z{fp_from_fd(r[4]), fp_from_fd(r[5])};
-    const Fp ni = k ? fp_mul_i(inv, pre[k - 1]) : inv;  // 1 / norm(Z)
+    const bool in = i < B;
+    const Fd* r = hf + HCF * (in ? i : 0) + HCF_A;
     G2A h{fp2_zero(), fp2_zero(), true};
-    if (!zero[k]) {
+    if (in && !zero[k]) {
+      const Fp2 Z{fp_from_fd(r[4]), fp_from_fd(r[5])};
+      const Fp ni = k ? fp_mul_i(inv, pre[k ? k - 1 : 0]) : inv;  // 1 / norm(Z)
       inv = k ? fp_mul_i(inv, fp2_norm(Z)) : inv;
       const Fp2 X{fp_from_fd(r[0]), fp_from_fd(r[1])}, Y{fp_from_fd(r[2]), fp_from_fd(r[3])};
       const Fp2 zi{fp_mul_i(Z.c0, ni), fp_neg(fp_mul_i(Z.c1, ni))};
       h = G2A{f2mul(X, zi), f2mul(Y, zi), false};
     }
-    H[i] = h;
-  }
+    if (in) H[i] = h;
+  }, std::make_integer_sequence<int, AFF_K2>{});
 }
 
 // ---------------------------------------------- hash_to_G2 on lane pairs --
@@ -331,7 +364,7 @@ static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs
     hipLaunchKernelGGL(k_h2c_sswu_iso2<false>, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, status, hf, flag);
   hipLaunchKernelGGL(k_g2x_pre1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
   hipLaunchKernelGGL(k_g2x_post1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
-  hipLaunchKernelGGL(k_h2c_affine_b, dim3(nblk(B, 64 * AFF_K)), dim3(64), 0, st, B, status, hf, H);
+  hipLaunchKernelGGL(k_h2c_affine_b, dim3(nblk(B, 64 * AFF_K2)), dim3(64), 0, st, B, status, hf, H);
   return hipGetLastError();
 }
 

@@ -33,8 +33,11 @@
 
 namespace bls {
 
+// 14 digits + 6 pad words: 80 B, so slot s starts in 16-B bank group (5 s) mod 16 and the 16-B accesses of lanes
+// reading different slots spread over the banks (at 64 B every fourth slot shared a group: 54.9 % of the kernel's
+// LDS cycles were bank conflicts, profiles/r03s_pmc_lds.md -- the layout that fixed the VM slots)
 struct alignas(16) FeSlot {
-  uint32_t d[16];  // 14 digits + 2 pad words (64 B: four 16-B LDS accesses)
+  uint32_t d[20];
 };
 
 // slot of a table reference: frame 0 absolute (products, temporaries, constants), 1/2/3 the banks A/B/D

@@ -65,6 +65,20 @@ BLS_HDNI bool fp2_sqrt_lane(Fp2& out, const Fp2& a) {
   return true;
 }
 
+// fp2_sqrt_lane inlined (the signature-decode kernel: the out-of-line call cost it a call frame of private memory)
+BLS_HD bool fp2_sqrt_lane_i(Fp2& out, const Fp2& a) {
+  if (fp_is_zero(a.c1)) {
+    const Fp s = fp_sqrt_cand(a.c0);
+    out = fp_eq(fp_sqr_i(s), a.c0) ? Fp2{s, fp_zero()} : Fp2{fp_zero(), s};
+    return true;
+  }
+  const Fp nrm = fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1));
+  const Fp n = fp_sqrt_cand(nrm);
+  if (!fp_eq(fp_sqr_i(n), nrm)) return false;
+  out = fp2_sqrt_from_norm_root(a, n);
+  return true;
+}
+
 BLS_HD int fp2_sgn0_lane(const Fp2& a_mont) {
   Fp one = fp_zero();
   one.l[0] = 1;
@@ -199,6 +213,46 @@ BLS_HDNI int g2_decompress_lane(G2A& out, const uint8_t* b) {
   Fp2 y;
   if (!fp2_sqrt_lane(y, rhs)) return DEC_NOT_ON_CURVE;
   if (fp2_lex_largest(y) != a_flag) y = fp2_neg(y);
+  out.x = xm;
+  out.y = y;
+  return DEC_OK;
+}
+
+constexpr Fp FP_RAW_ONE = {{1u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}};  // a R^-1 = a out of Montgomery form
+
+// g2_decompress_lane for 4-byte-aligned signatures, inline and call-free: word loads instead of a byte buffer,
+// fp_mul_i by R^2 instead of the out-of-line fp_to_mont, fp2_sqrt_lane_i.  Same statuses and points.
+__device__ __forceinline__ int g2_decompress_lane_w(G2A& out, const uint8_t* b) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(b);
+  Fp x1, x0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    x1.l[11 - k] = __builtin_bswap32(w[k]);
+    x0.l[11 - k] = __builtin_bswap32(w[12 + k]);
+  }
+  const uint32_t f = x1.l[11] >> 24;
+  const bool c_flag = f & 0x80, b_flag = f & 0x40, a_flag = f & 0x20;
+  x1.l[11] &= 0x1fffffffu;
+  out.inf = false;
+  if (!c_flag) return DEC_BAD_FLAGS;
+  const bool x_zero = fp_is_zero(x1) && fp_is_zero(x0);
+  if (b_flag != x_zero) return DEC_BAD_FLAGS;
+  if (x_zero) {
+    if (a_flag) return DEC_BAD_FLAGS;
+    out.inf = true;
+    out.x = fp2_zero();
+    out.y = fp2_zero();
+    return DEC_INFINITY;
+  }
+  if (!raw_lt_p(x1) || !raw_lt_p(x0)) return DEC_NOT_FIELD;
+  const Fp2 xm{fp_mul_i(x0, FP_R2), fp_mul_i(x1, FP_R2)};
+  const Fp2 rhs = fp2_add(f2mul(f2sqr(xm), xm), FP2_B2);
+  Fp2 y;
+  if (!fp2_sqrt_lane_i(y, rhs)) return DEC_NOT_ON_CURVE;
+  // fp2_lex_largest inline (the out-of-line one is a call frame of private memory)
+  const Fp y0 = fp_mul_i(y.c0, FP_RAW_ONE), y1 = fp_mul_i(y.c1, FP_RAW_ONE);
+  const bool largest = !fp_is_zero(y1) ? raw_gt_half(y1) : raw_gt_half(y0);
+  if (largest != a_flag) y = fp2_neg(y);
   out.x = xm;
   out.y = y;
   return DEC_OK;
