@@ -464,8 +464,13 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
-  LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, hf, Q, flag));
-  CK(h2c_fallback(ctx, st2, 1, d_msg, d_offs, flag, Q));
+  // 32-byte messages (every signing root) take the register-resident expand_message_xmd of the FAV batches
+  const uint64_t* h_offs = msg_len == 32 ? nullptr : d_offs;
+  if (h_offs)
+    LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, hf, Q, flag));
+  else
+    LK(launch_h2c(st2, 1, d_msg, nullptr, hf, Q, flag));
+  CK(h2c_fallback(ctx, st2, 1, d_msg, h_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
   HIPCK(hipEventRecord(J.ev_sig, st3));
@@ -544,8 +549,13 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
     int* d_flag;
     SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
     SCR(S_AV_FLAG, n, d_flag);
-    LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_hf, Q, d_flag));
-    CK(h2c_fallback(ctx, ctx->j->stream, n, d_msgs, d_offs, d_flag, Q));
+    bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
+    for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
+    if (m32)
+      LK(launch_h2c(ctx->j->stream, n, d_msgs, nullptr, d_hf, Q, d_flag));
+    else
+      LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_hf, Q, d_flag));
+    CK(h2c_fallback(ctx, ctx->j->stream, n, d_msgs, m32 ? nullptr : d_offs, d_flag, Q));
   }
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->j->stream, P + n);
   LK(hipGetLastError());

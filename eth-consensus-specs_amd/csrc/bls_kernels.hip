@@ -74,16 +74,6 @@ __global__ void __launch_bounds__(64) k_key_validate(const uint8_t* pks48, size_
   ok[i] = v;
 }
 
-__global__ void __launch_bounds__(64) k_sig_validate(const uint8_t* sigs96, size_t n, G2A* out, int* ok) {
-  size_t i = gtid();
-  if (i >= n) return;
-  G2A a;
-  int v = sig_validate(a, sigs96 + 96 * i);
-  if (!v) a = G2A{fp2_zero(), fp2_zero(), true};
-  out[i] = a;
-  ok[i] = v;
-}
-
 // ------------------------------------------------------------ reductions --
 // Sum of affine G1 points (only entries with ok != 0 when ok is given) into
 // one Jacobian partial per workgroup.
@@ -486,11 +476,6 @@ static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1
 hipError_t launch_key_validate(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok) {
   if (!n) return hipSuccess;
   LAUNCH(k_key_validate, nblk(n, 64), 64, st, pks, n, out, ok);
-  return hipSuccess;
-}
-hipError_t launch_sig_validate(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok) {
-  if (!n) return hipSuccess;
-  LAUNCH(k_sig_validate, nblk(n, 64), 64, st, sigs, n, out, ok);
   return hipSuccess;
 }
 

@@ -38,6 +38,23 @@ for s in $STEPS; do
         "profiles/${TAG}_kernel_stats.md (rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu)" > /dev/null; fi
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
       tail -2 "$OUT/prof.log" ;;
+    percall)
+      timeout -k 10 120 python3 tools/percall_probe.py > "$OUT/percall.json" 2> "$OUT/percall.err" \
+        || { tail -20 "$OUT/percall.err"; exit 1; }
+      cat "$OUT/percall.json"
+      REPS=5 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/pcprof" -o run -- \
+        python3 tools/percall_probe.py > "$OUT/pcprof.log" 2>&1 || { tail -20 "$OUT/pcprof.log"; exit 1; }
+      db=$(find "$OUT/pcprof" -name '*.db' | head -n 1)
+      if [ -n "$db" ]; then python3 tools/rocprof_summary.py "$db" "$OUT/percall_kernel_stats.md" "$OUT/percall_avg.json" \
+        "profiles/${TAG}_percall_kernel_stats.md (rocprofv3 --kernel-trace --stats -- python3 tools/percall_probe.py)" > /dev/null; fi
+      find "$OUT/pcprof" -name '*kernel_stats.csv' -exec cp {} "$OUT/percall_kernel_stats.csv" \; ;;
+    c3tl)
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/c3tl" -o run -- \
+        python3 bench.py --config c3 --steps 25 --warmup 2 --no-cpu --no-percall --no-parity --no-e2e --no-profile \
+        > "$OUT/c3tl.log" 2>&1 || { tail -20 "$OUT/c3tl.log"; exit 1; }
+      tail -1 "$OUT/c3tl.log"
+      db=$(find "$OUT/c3tl" -name '*.db' | head -n 1)
+      if [ -n "$db" ]; then python3 tools/timeline.py "$db" k_miller_acc4 2 24 > "$OUT/c3_timeline.txt" 2>&1 || true; head -12 "$OUT/c3_timeline.txt"; fi ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
