@@ -109,6 +109,7 @@ _SIGS = {
     "bls_set_entropy_source": (_ip, [ctypes.c_char_p]),
     "bls_test_force_h2c_fallback": (_ip, [_vp, _u8p, _sz]),
     "bls_test_hash_to_g2_batch": (_ip, [_vp, _u8p, _sz, _vp]),
+    "bls_test_wide_selftest": (_ip, [_vp, _u8p, _sz, _vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -762,6 +762,22 @@ int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uin
   return 0;
 }
 
+// Device self-test of the wavefront-cooperative products (bls_wide.h) against the lane form: nw waves, each on four
+// inputs (48-byte big-endian integers < p); bad[w] = bitmask of the forms whose results differ (0 = all equal).
+int bls_test_wide_selftest(bls_ctx* ctx, const uint8_t* in48, size_t nw, int32_t* bad) {
+  API_ENTER(ctx);
+  if ((!in48 || !bad) && nw) return BLS_E_ARG;
+  if (!nw) return 0;
+  uint8_t* d_in;
+  int* d_bad;
+  SCR(S_IN0, 4 * 48 * nw, d_in);
+  SCR(S_OK, nw, d_bad);
+  CK(h2d(ctx, d_in, in48, 4 * 48 * nw));
+  LK(launch_wide_selftest(ctx->j->stream, nw, d_in, d_bad));
+  CK(d2h(ctx, bad, d_bad, nw * sizeof(int)));
+  return 0;
+}
+
 // ------------------------------------------------------------- registry --
 // Decode + KeyValidate n keys into reg[first ..] (valid[] = the verdicts).
 static int registry_fill(bls_ctx* ctx, const uint8_t* pks48, size_t n, size_t first, uint8_t* out_valid) {

@@ -89,4 +89,7 @@ hipError_t launch_pt_msm(hipStream_t st, int group, const void* P, const uint8_t
 hipError_t launch_gt_final_exp(hipStream_t st, const Fp12* f, uint8_t* out576);
 hipError_t launch_gt_mul(hipStream_t st, const uint8_t* a, const uint8_t* b, uint8_t* out);
 
+// wavefront-cooperative arithmetic (bls_wide.hip)
+hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad);
+
 }  // namespace bls

@@ -1,0 +1,267 @@
+// Wavefront-cooperative ("wide") Fp arithmetic for the latency-bound one-item
+// chains of the per-call path (north_star (a): multi-limb carries across the
+// lanes of a wavefront).
+//
+// Why.  In the lane form (bls_fq.h) one lane owns a whole value and a product
+// is ~500 wave instructions: a chain of N dependent products takes N x ~1 us
+// whatever the other 63 lanes do.  That is the right trade for batches (64
+// items per wave) and the wrong one for a single Verify, whose hash_to_G2,
+// signature check and key check are chains of thousands of dependent products.
+//
+// Layout ("D layout").  A value is 14 radix-2^29 digits of the Montgomery form
+// (R = 2^406, the same representation as bls_fq.h) spread over the lanes of a
+// 32-lane half-wave: lane k of the half holds digit (k mod 16) when k mod 16 <
+// 14, else 0 -- i.e. both 16-lane rows of the half hold the digits.  The two
+// halves of a wave hold two independent values (two items, or two chains of one
+// item), so every operation below runs both at once.  One VGPR per value.
+//
+// Product x y R^-1 mod p (wmul / wdot2), per half:
+//   1. column sums: lane k accumulates c_k = sum_i x_i y_{k-i} in 64 bits --
+//      x_i is a row broadcast (DPP row_newbcast:i; both rows hold x), y walks up
+//      one lane per step (DPP wave_shr:1): 14 steps of (two DPP moves, one
+//      v_mad_u64_u32).
+//   2. carry-save normalisation (wnorm64: two rounds of d_k = (d_k mod 2^29) +
+//      (d_{k-1} >> 29), one DPP move each): digits <= 2^29 + 64, same value.
+//   3. m = (T mod R) (-p^-1) mod R as a 14-column half product by the constant
+//      NINV29 (scalar operands), normalised, lanes >= 14 dropped (mod R).
+//   4. T + m p (14 more steps), normalised: the low 14 digits then sum to 0 or
+//      exactly R (they are = 0 mod R and below 2 R), so the carry into digit 14
+//      is "any low digit nonzero" -- one wave ballot, no carry chain.
+//   5. digits 14..27 move down to lanes 0..13 of both rows (ds_bpermute).
+// ~140 wave instructions per product pair instead of ~500 per lane product:
+// ~3.5x lower latency per product, ~8x per Fp2 product (wdot2 forms a whole
+// Fp2 coefficient with one reduction).  Nothing is sequential across digits
+// except the DPP walk; no lane ever holds more than one digit of a value.
+//
+// Bounds ("W form"): digits <= 2^29 + 64 (digit 13 small), value < 2.0001 p for
+// products whose operand values multiply to < p R (R/p ~ 2^25.3).  Column sums
+// stay below 2^63 for one product of W-form operands and for wdot2 (28 terms);
+// sums of two W values must be normalised (wnorm) before they enter a product.
+// Subtractions add Q29_K1 = 64 p in borrowed digits (each >= 2^29 + 2^25), so the
+// subtrahend must be a W value below 62 p.
+//
+// All control flow is uniform across the wave; results are checked against the
+// lane form on the device (bls_test_wide_selftest, tests/test_gpu_percall.py).
+#pragma once
+#include <utility>
+
+#include "bls_fq.h"
+
+namespace bls {
+namespace wide {
+
+constexpr uint32_t WM = 0x1fffffffu;
+// -p^-1 mod 2^406 in radix 2^29 (digit 0 is P29_NINV); n' p = -1 mod R is checked in tests/test_hostcheck.py
+constexpr uint32_t NINV29[14] = {0x1ffcfffdu, 0x0f9fffe7u, 0x1444fa22u, 0x15b725b3u, 0x10b48286u,
+                                 0x17786471u, 0x0d305bbcu, 0x01d1d65bu, 0x1819eccau, 0x1713467au,
+                                 0x1a2cc5bfu, 0x1d55f928u, 0x0b06106fu, 0x1f13d067u};
+
+__device__ __forceinline__ int wlane() { return (int)(threadIdx.x & 63u); }
+__device__ __forceinline__ int wpos() { return (int)(threadIdx.x & 31u); }  // lane within the half
+__device__ __forceinline__ int wdig() { return (int)(threadIdx.x & 15u); }  // digit index in D layout
+__device__ __forceinline__ int whalf() { return (int)((threadIdx.x >> 5) & 1u); }
+
+// DPP wave_shr:1 -- lane l gets lane l - 1, lane 0 gets 0 (lane 32 gets lane 31, which is always 0 here)
+__device__ __forceinline__ uint32_t shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: invalid source -> 0
+}
+// DPP row_newbcast:I -- every lane of a 16-lane row gets lane I of that row
+template <int I>
+__device__ __forceinline__ uint32_t rbc(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + I, 0xF, 0xF, true);
+}
+template <class F, int... I>
+__device__ __forceinline__ void for14_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <class F>
+__device__ __forceinline__ void for14(F&& f) {
+  for14_(f, std::make_integer_sequence<int, 14>{});
+}
+
+// d_k = (d_k mod 2^29) + (d_{k-1} >> 29): same value, digits <= 2^29 - 1 + (max digit >> 29)
+__device__ __forceinline__ uint32_t wnorm(uint32_t d) { return (d & WM) + shr1(d >> 29); }
+
+// 64-bit column sums (< 2^63) -> 32-bit digits <= 2^29 + 64, same value (two carry-save rounds)
+__device__ __forceinline__ uint32_t wnorm64(uint64_t c) {
+  const uint64_t h = c >> 29;  // < 2^34
+  const uint64_t hs = ((uint64_t)shr1((uint32_t)(h >> 32)) << 32) | shr1((uint32_t)h);
+  const uint64_t c1 = (uint64_t)((uint32_t)c & WM) + hs;  // < 2^35
+  return ((uint32_t)c1 & WM) + shr1((uint32_t)(c1 >> 29));
+}
+
+// acc += x y as column sums (lane k of the half: sum_i x_i y_{k-i}); x, y in D layout
+__device__ __forceinline__ void wmac(uint64_t& acc, uint32_t x, uint32_t y) {
+  uint32_t s = wpos() < 14 ? y : 0u;  // y's digits of row 0 only
+  for14([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (i) s = shr1(s);
+    acc += (uint64_t)rbc<i>(x) * s;
+  });
+}
+
+// Montgomery reduction of column sums (< 2^63, value T < p R): T R^-1 mod p in W form (value < 2.0001 p)
+__device__ __forceinline__ uint32_t wredc(uint64_t acc) {
+  const int k = wpos();
+  const uint32_t t = wnorm64(acc);
+  uint64_t am = 0;
+  uint32_t s = k < 14 ? t : 0u;
+  for14([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (i) s = shr1(s);
+    am += (uint64_t)NINV29[i] * s;
+  });
+  const uint32_t mn = wnorm64(am);
+  const uint32_t m = k < 14 ? mn : 0u;  // m = -T p^-1 mod R, < R (1 + 2^-23)
+  uint64_t au = t;
+  s = m;
+  for14([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (i) s = shr1(s);
+    au += (uint64_t)P29[i] * s;
+  });
+  const uint32_t u = wnorm64(au);
+  // the low 14 digits sum to 0 or R: the carry into digit 14 is "any of them nonzero"
+  const uint64_t bal = __builtin_amdgcn_ballot_w64(k < 14 && u != 0u);
+  const bool lowc = ((bal >> (threadIdx.x & 32u)) & 0x3fffull) != 0;
+  const uint32_t u2 = u + ((k == 14 && lowc) ? 1u : 0u);
+  const int j = wdig();
+  const int src = (int)(threadIdx.x & 32u) + (j < 14 ? 14 + j : 31);  // lane 31 of a half is always 0
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)u2);
+}
+
+__device__ __forceinline__ uint32_t wmul(uint32_t x, uint32_t y) {
+  uint64_t a = 0;
+  wmac(a, x, y);
+  return wredc(a);
+}
+__device__ __forceinline__ uint32_t wsqr(uint32_t x) { return wmul(x, x); }
+// (x y + u v) R^-1 with one reduction
+__device__ __forceinline__ uint32_t wdot2(uint32_t x, uint32_t y, uint32_t u, uint32_t v) {
+  uint64_t a = 0;
+  wmac(a, x, y);
+  wmac(a, u, v);
+  return wredc(a);
+}
+
+// per-lane constants of a kernel: the subtraction constant 64 p (Q29_K1) and R mod p (one) in D layout
+struct WK {
+  uint32_t k1, one, zero;
+};
+__device__ __forceinline__ WK wk_init() {
+  const int j = wdig();
+  const Fq o = fq_unpack(FP_ONE);
+  uint32_t k1 = 0, one = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    k1 = j == i ? Q29_K1[i] : k1;
+    one = j == i ? o.d[i] : one;
+  }
+  return WK{k1, one, 0u};
+}
+
+__device__ __forceinline__ uint32_t wadd(uint32_t a, uint32_t b) { return wnorm(a + b); }
+// a - b (b a W value below 62 p): a + 64 p - b digit-wise, normalised
+__device__ __forceinline__ uint32_t wsub(const WK& K, uint32_t a, uint32_t b) { return wnorm(a + (K.k1 - b)); }
+__device__ __forceinline__ uint32_t wneg(const WK& K, uint32_t b) { return wnorm(K.k1 - b); }
+// small multiple of a W value, normalised (k <= 7 per step keeps a digit below 2^32)
+template <uint32_t KM>
+__device__ __forceinline__ uint32_t wmuls(uint32_t a) {
+  if constexpr (KM <= 7u)
+    return wnorm(a * KM);
+  else
+    return wmuls<KM / 2>(wmuls<2>(a)) + (KM & 1u ? a : 0u);  // KM even only on the paths used (8, 12, ...)
+}
+
+// ---- conversions (kernel edges; lane-local work, not on the chain) ----------
+// this half's value as a lane-local Fq (every lane of the half gets all 14 digits)
+__device__ __forceinline__ Fq w_to_fq(uint32_t v) {
+  Fq r;
+  const bool hi = whalf() != 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+    const uint32_t up = (uint32_t)__builtin_amdgcn_readlane((int)v, 32 + i);
+    r.d[i] = hi ? up : lo;
+  }
+  return r;
+}
+// a lane-local Fq (the same in every lane of a half, or different per half) -> D layout
+__device__ __forceinline__ uint32_t w_from_fq(const Fq& a) {
+  const int j = wdig();
+  uint32_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) v = j == i ? a.d[i] : v;
+  return v;
+}
+__device__ __forceinline__ uint32_t w_from_fp(const Fp& a) { return w_from_fq(fq_unpack(a)); }
+// canonical packed Montgomery Fp of this half's value
+__device__ __forceinline__ Fp w_to_fp(uint32_t v) { return fq_pack(w_to_fq(v)); }
+__device__ __forceinline__ bool w_is_zero(uint32_t v) { return fp_is_zero(w_to_fp(v)); }
+__device__ __forceinline__ bool w_eq(const WK& K, uint32_t a, uint32_t b) { return w_is_zero(wsub(K, a, b)); }
+// the other half's value (lane l gets lane l ^ 32)
+__device__ __forceinline__ uint32_t wswap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ 32u) & 63u) << 2, (int)v);
+}
+
+// a^e for a fixed exponent (little-endian u32 limbs, bit nbits-1 set), sliding window w = 3 (as fq_pow_w3)
+__device__ __forceinline__ uint32_t wpow(uint32_t a, const uint32_t* e, int nbits) {
+  const uint32_t a2 = wsqr(a);
+  const uint32_t t1 = a, t3 = wmul(t1, a2), t5 = wmul(t3, a2), t7 = wmul(t5, a2);
+  uint32_t r = t1;
+  bool started = false;
+  int i = nbits - 1;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      r = wsqr(r);
+      --i;
+      continue;
+    }
+    int j = i - 2 < 0 ? 0 : i - 2;
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) ++j;
+    uint32_t w = 0;
+    for (int k = i; k >= j; --k) w = (w << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
+    const uint32_t m = w == 1u ? t1 : (w == 3u ? t3 : (w == 5u ? t5 : t7));
+    if (!started) {
+      r = m;
+      started = true;
+    } else {
+      for (int k = i; k >= j; --k) r = wsqr(r);
+      r = wmul(r, m);
+    }
+    i = j - 1;
+  }
+  return r;
+}
+
+// ---- Fp2 in pair form: (c0, c1) as two D-layout values per half -----------
+struct W2 {
+  uint32_t c0, c1;
+};
+__device__ __forceinline__ W2 w2add(W2 a, W2 b) { return W2{wadd(a.c0, b.c0), wadd(a.c1, b.c1)}; }
+__device__ __forceinline__ W2 w2sub(const WK& K, W2 a, W2 b) { return W2{wsub(K, a.c0, b.c0), wsub(K, a.c1, b.c1)}; }
+__device__ __forceinline__ W2 w2neg(const WK& K, W2 a) { return W2{wneg(K, a.c0), wneg(K, a.c1)}; }
+template <uint32_t KM>
+__device__ __forceinline__ W2 w2muls(W2 a) {
+  return W2{wmuls<KM>(a.c0), wmuls<KM>(a.c1)};
+}
+__device__ __forceinline__ W2 w2conj(const WK& K, W2 a) { return W2{a.c0, wneg(K, a.c1)}; }
+// c0 = a0 b0 + a1 (64p - b1), c1 = a0 b1 + a1 b0: one reduction per coefficient
+__device__ __forceinline__ W2 w2mul(const WK& K, W2 a, W2 b) {
+  return W2{wdot2(a.c0, b.c0, a.c1, wneg(K, b.c1)), wdot2(a.c0, b.c1, a.c1, b.c0)};
+}
+// (a0 + a1)(a0 - a1), 2 a0 a1
+__device__ __forceinline__ W2 w2sqr(const WK& K, W2 a) {
+  return W2{wmul(wadd(a.c0, a.c1), wsub(K, a.c0, a.c1)), wmul(a.c0, wadd(a.c1, a.c1))};
+}
+__device__ __forceinline__ W2 w2mulfp(W2 a, uint32_t b) { return W2{wmul(a.c0, b), wmul(a.c1, b)}; }
+// a (1 + u): the Fp2 non-residue xi
+__device__ __forceinline__ W2 w2xi(const WK& K, W2 a) { return W2{wsub(K, a.c0, a.c1), wadd(a.c0, a.c1)}; }
+__device__ __forceinline__ W2 w2_from_fp2(const Fp2& a) { return W2{w_from_fp(a.c0), w_from_fp(a.c1)}; }
+__device__ __forceinline__ Fp2 w2_to_fp2(W2 a) { return Fp2{w_to_fp(a.c0), w_to_fp(a.c1)}; }
+__device__ __forceinline__ bool w2_is_zero(W2 a) { return w_is_zero(a.c0) && w_is_zero(a.c1); }
+__device__ __forceinline__ W2 w2swap(W2 a) { return W2{wswap(a.c0), wswap(a.c1)}; }
+__device__ __forceinline__ W2 w2sel(bool c, W2 a, W2 b) { return W2{c ? a.c0 : b.c0, c ? a.c1 : b.c1}; }
+
+}  // namespace wide
+}  // namespace bls

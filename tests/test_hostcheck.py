@@ -465,3 +465,16 @@ def test_sswu_rare_case_flagged():
         assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
         out = H.call("hc_map_to_curve_lane", H.fp2_b(u), out=192)
         assert (H.b_fp2(out[:96]), H.b_fp2(out[96:])) == O.map_to_curve_sswu(u)
+
+
+def test_wide_montgomery_constant():
+    """bls_wide.h NINV29 = -p^-1 mod 2^406 in radix 2^29 (the whole-word constant of its parallel reduction)."""
+    import os
+    import re
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "eth-consensus-specs_amd", "csrc", "bls_wide.h")).read()
+    body = re.search(r"NINV29\[14\] = \{([^}]*)\}", src).group(1)
+    d = [int(x.strip().rstrip("u"), 16) for x in body.split(",")]
+    n = sum(x << (29 * i) for i, x in enumerate(d))
+    R = 1 << 406
+    assert len(d) == 14 and all(x < (1 << 29) for x in d) and (n * O.P + 1) % R == 0
