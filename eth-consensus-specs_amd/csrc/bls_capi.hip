@@ -427,6 +427,8 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
 // exponentiation check.  Every chain that can be spread over a workgroup is
 // (the h2c and pairing phases); only the square roots and subgroup checks run
 // one lane each.
+constexpr size_t WIDE_H2C_MAX = 512;  // AggregateVerify: one wave per message up to this many
+
 static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
                           const uint8_t* sig96) {
   Job& J = *ctx->j;
@@ -464,12 +466,11 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
-  // 32-byte messages (every signing root) take the register-resident expand_message_xmd of the FAV batches
+  // one wave of wavefront-cooperative arithmetic for the one message (bls_wide.h); 32-byte messages (every
+  // signing root) take the register-resident expand_message_xmd
   const uint64_t* h_offs = msg_len == 32 ? nullptr : d_offs;
-  if (h_offs)
-    LK(launch_h2c_msgs(st2, 1, d_msg, d_offs, hf, Q, flag));
-  else
-    LK(launch_h2c(st2, 1, d_msg, nullptr, hf, Q, flag));
+  (void)hf;
+  LK(launch_h2c_wide(st2, 1, d_msg, h_offs, Q, flag));
   CK(h2c_fallback(ctx, st2, 1, d_msg, h_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
@@ -551,7 +552,9 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
     SCR(S_AV_FLAG, n, d_flag);
     bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
     for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
-    if (m32)
+    if (n <= WIDE_H2C_MAX)  // a few messages: one wave each, lower latency than the lane kernels' chains
+      LK(launch_h2c_wide(ctx->j->stream, n, d_msgs, m32 ? nullptr : d_offs, Q, d_flag));
+    else if (m32)
       LK(launch_h2c(ctx->j->stream, n, d_msgs, nullptr, d_hf, Q, d_flag));
     else
       LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_hf, Q, d_flag));
@@ -739,6 +742,28 @@ __global__ void k_g2_compress_many(size_t n, const G2A* in, uint8_t* out96) {
 
 // hash_to_G2 of n 32-byte messages (DST POP) through the FAV batch's lane kernels and fallback routing
 // (launch_h2c + h2c_fallback, exactly as bls_fav_* run them), compressed: out96[96 i ..] = H(m_i).
+// the same through the one-wave-per-message kernel of the per-call path (launch_h2c_wide + h2c_fallback)
+int bls_test_hash_to_g2_wide(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96) {
+  API_ENTER(ctx);
+  if ((!msgs32 || !out96) && n) return BLS_E_ARG;
+  if (!n) return 0;
+  uint8_t *d_m, *d_out;
+  G2A* H;
+  int* flag;
+  SCR(S_IN0, 32 * n, d_m);
+  SCR(S_IN2, 96 * n, d_out);
+  SCR(S_AV_FLAG, n, flag);
+  SCR(S_G2A, n, H);
+  hipStream_t st = ctx->j->stream;
+  CK(h2d(ctx, d_m, msgs32, 32 * n));
+  LK(launch_h2c_wide(st, n, d_m, nullptr, H, flag));
+  CK(h2c_fallback(ctx, st, n, d_m, nullptr, flag, H));
+  hipLaunchKernelGGL(k_g2_compress_many, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, H, d_out);
+  LK(hipGetLastError());
+  CK(d2h(ctx, out96, d_out, 96 * n));
+  return 0;
+}
+
 int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96) {
   API_ENTER(ctx);
   if ((!msgs32 || !out96) && n) return BLS_E_ARG;

@@ -4,10 +4,17 @@
 #include "bls_kernels.h"
 #include "bls_lane.h"
 #include "bls_wide.h"
+#include "bls_wide_g2.h"
+#include "bls_xmd32.h"
+#include "bls_h2c.h"
 
 namespace bls {
 
 using namespace wide;
+
+__device__ static const uint8_t DST_POP_WIDE[43] = {
+    'B', 'L', 'S', '_', 'S', 'I', 'G', '_', 'B', 'L', 'S', '1', '2', '3', '8', '1', 'G', '2', '_', 'X', 'M', 'D',
+    ':', 'S', 'H', 'A', '-', '2', '5', '6', '_', 'S', 'S', 'W', 'U', '_', 'R', 'O', '_', 'P', 'O', 'P', '_'};
 
 // Self-test: wave w takes a[4w .. 4w+4) (canonical Montgomery Fp): half h multiplies a[4w + 2h] by a[4w + 2h + 1]
 // in every wide form and compares with the lane form; bad[w] = bitmask of the forms that differ.
@@ -52,6 +59,56 @@ __global__ void __launch_bounds__(64) k_wide_selftest(size_t nw, const uint8_t* 
   const int mh = m;
   const int mo = __builtin_amdgcn_readlane(mh, 32);
   if (threadIdx.x == 0) bad[w] = mh | (mo << 10);
+}
+
+// hash_to_G2 of item blockIdx.x on one wave (per-call path): hash_to_field on every lane (uniform), the SSWU map
+// and 3-isogeny of u_0 in half 0 and of u_1 in half 1, their sum, the cofactor clearing
+//   H = [x^2 - x - 1] Q + [x - 1] psi(Q) + psi^2(2 Q)  as  M = [|x|] Q,  A' = M - psi(Q),
+//   C = psi^2(2 Q) - psi(Q) + M - Q,  H = C + [|x|] A'   (A' = -A of k_g2x_pre1t / k_g2x_post1t)
+// in both halves (two Jacobian representations of the same points), and the affine H from half 0.  flag[i] = 1
+// for the cases the fallback recomputes (SSWU `rare`, a vanishing isogeny denominator, an exceptional addition).
+// msgs: 32-byte messages msgs[32 i ..] (offs == nullptr) or msgs[offs[i] .. offs[i+1]).
+__global__ void __launch_bounds__(64) k_h2c_wide(size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H,
+                                                 int* flag) {
+  const size_t i = blockIdx.x;
+  if (i >= B) return;
+  const WKG K = wkg_init();
+  Fp2 u[2];
+  if (offs)
+    hash_to_field_fp2(u, msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_WIDE, 43);
+  else
+    hash_to_field_fp2_m32(u, msgs + 32 * i);
+  const bool hi = whalf() != 0;
+  const Fp2 uh{fp_select(hi, u[1].c0, u[0].c0), fp_select(hi, u[1].c1, u[0].c1)};
+  W2 x, y;
+  bool rare = false, izero = false, exc = false;
+  sswu_w(K, uh, x, y, rare);
+  const J2W P = iso_w(K, x, y, izero);
+  const J2W Po{w2swap(P.x), w2swap(P.y), w2swap(P.z)};
+  const J2W Q = j2w_add(K, P, Po, exc);
+  const W2 cx = w2const(PSI_CX), cy = w2const(PSI_CY);
+  const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
+  const J2W M = j2w_mul_xabs(K, Q, exc);
+  const J2W npq = j2w_neg(K, j2w_psi(K, Q, cx, cy));
+  const J2W Ap = j2w_add(K, M, npq, exc);
+  J2W C = j2w_add(K, j2w_psi2(K, j2w_dbl(K, Q), c2x, c2y), npq, exc);
+  C = j2w_add(K, C, M, exc);
+  C = j2w_add(K, C, j2w_neg(K, Q), exc);
+  const J2W M2 = j2w_mul_xabs(K, Ap, exc);
+  const J2W Hj = j2w_add(K, C, M2, exc);
+  const G2A h = j2w_to_aff(K, Hj);
+  const int bad = (rare | izero | exc) ? 1 : 0;
+  const int bad_any = __builtin_amdgcn_readlane(bad, 0) | __builtin_amdgcn_readlane(bad, 32);
+  if (threadIdx.x == 0) {
+    H[i] = h;
+    flag[i] = bad_any;
+  }
+}
+
+hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_h2c_wide, dim3((unsigned)B), dim3(64), 0, st, B, msgs, offs, H, flag);
+  return hipGetLastError();
 }
 
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad) {

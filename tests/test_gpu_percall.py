@@ -25,3 +25,49 @@ def test_wide_products_match_lane_form():
     bad = np.zeros(nw, dtype=np.int32)
     ctx.check(ctx.lib.bls_test_wide_selftest(ctx.h, buf, nw, bad.ctypes.data_as(ctypes.c_void_p)))
     assert not bad.any(), [(int(w), hex(int(bad[w]))) for w in np.nonzero(bad)[0][:8]]
+
+
+def test_h2c_wide_matches_oracle():
+    """hash_to_G2 through the one-wave-per-message kernel of the per-call path (SSWU + isogeny in the two halves,
+    cofactor clearing in wide Jacobian arithmetic) equals the C oracle's and the FAV batch kernels' points."""
+    import ctypes
+    import hashlib
+
+    from bls_mi355x import _native
+    from oracle import bls_oracle_c as OC
+
+    ctx = _native.context()
+    msgs = [hashlib.sha256(b"wide" + j.to_bytes(4, "little")).digest() for j in range(70)]
+    msgs += [bytes(32), b"\xff" * 32]
+    n = len(msgs)
+    wide = ctypes.create_string_buffer(96 * n)
+    ctx.check(ctx.lib.bls_test_hash_to_g2_wide(ctx.h, b"".join(msgs), n, wide))
+    lane = ctypes.create_string_buffer(96 * n)
+    ctx.check(ctx.lib.bls_test_hash_to_g2_batch(ctx.h, b"".join(msgs), n, lane))
+    assert wide.raw == lane.raw
+    for j in list(range(0, n, 7)) + [n - 2, n - 1]:
+        assert wide.raw[96 * j: 96 * j + 96] == OC.hash_to_g2(msgs[j]), j
+
+
+@pytest.mark.parametrize("mlen", [0, 1, 31, 32, 33, 100])
+def test_percall_verify_message_lengths(mlen):
+    """Per-call Verify / FastAggregateVerify / AggregateVerify with messages of every length class (the wide hash's
+    byte-streaming and 32-byte paths) against the C oracle's signatures: valid -> True, wrong message -> False."""
+    from bls_mi355x.backend import mi355x_bls as M
+    from oracle import bls_oracle_c as OC
+
+    msg = bytes((7 * k + mlen) & 0xFF for k in range(mlen))
+    other = bytes([0x5A]) + msg[1:] if mlen else b"\x01"
+    pk = OC.SkToPk(4242)
+    sig = OC.Sign(4242, msg)
+    assert M.Verify(pk, msg, sig) is True
+    assert M.Verify(pk, other, sig) is False
+    pks = [OC.SkToPk(k) for k in (11, 12, 13)]
+    agg = OC.Sign(11 + 12 + 13, msg)
+    assert M.FastAggregateVerify(pks, msg, agg) is True
+    assert M.FastAggregateVerify(pks[:2], msg, agg) is False
+    msgs = [msg + bytes([k]) for k in range(3)]
+    av = OC.Aggregate([OC.Sign(k, m) for k, m in zip((21, 22, 23), msgs)])
+    avpks = [OC.SkToPk(k) for k in (21, 22, 23)]
+    assert M.AggregateVerify(avpks, msgs, av) is True
+    assert M.AggregateVerify(avpks, [msgs[1], msgs[0], msgs[2]], av) is False
