@@ -473,7 +473,7 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   LK(launch_h2c_wide(st2, 1, d_msg, h_offs, Q, flag));
   CK(h2c_fallback(ctx, st2, 1, d_msg, h_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
-  LK(launch_sig_validate(st3, d_sig, 1, Q + 1, ok + n));
+  LK(launch_sig_validate_wide(st3, d_sig, 1, Q + 1, ok + n));
   HIPCK(hipEventRecord(J.ev_sig, st3));
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, P + 2);
   LK(hipGetLastError());

@@ -111,6 +111,87 @@ hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const 
   return hipGetLastError();
 }
 
+// Signature decode + G2 subgroup check of item blockIdx.x on one wave (per-call path; k_sig_validate semantics:
+// the identity encoding is accepted, every other failure is invalid).  Decoding up to the Montgomery x on every
+// lane (g2_decompress_lane_w's checks), then in wide arithmetic (both halves, the same chain): y^2 = x^3 + 4(1 + u)
+// by the norm square root (bls_lane.h fp2_sqrt_lane_i; the pure-Fp case, unreachable for x of a valid point with
+// probability ~2^-381, runs fp2_sqrt_lane_i on the lanes -- a wave-uniform branch), the sign, and
+// psi(sigma) == -[|x|] sigma through the wide Jacobian chain (an exceptional addition means a small order: reject).
+__global__ void __launch_bounds__(64) k_sig_validate_wide(const uint8_t* sigs96, size_t n, G2A* out, int* ok) {
+  const size_t i = blockIdx.x;
+  if (i >= n) return;
+  const WKG K = wkg_init();
+  const WK K1 = wk_of(K);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(sigs96 + 96 * i);
+  Fp x1, x0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    x1.l[11 - k] = __builtin_bswap32(w[k]);
+    x0.l[11 - k] = __builtin_bswap32(w[12 + k]);
+  }
+  const uint32_t f = x1.l[11] >> 24;
+  const bool c_flag = f & 0x80, b_flag = f & 0x40, a_flag = f & 0x20;
+  x1.l[11] &= 0x1fffffffu;
+  const bool x_zero = fp_is_zero(x1) && fp_is_zero(x0);
+  G2A s{fp2_zero(), fp2_zero(), true};
+  int v = 0;
+  // every condition below is wave-uniform (all lanes decode the same bytes)
+  if (c_flag && b_flag == x_zero) {
+    if (x_zero) {
+      v = a_flag ? 0 : 1;  // the identity encoding
+    } else if (raw_lt_p(x1) && raw_lt_p(x0)) {
+      const W2 xm = w2_from_fp2(Fp2{fp_mul_i(x0, FP_R2), fp_mul_i(x1, FP_R2)});
+      const W2 rhs = w2add(w2mul(K1, w2sqr(K1, xm), xm), w2const(FP2_B2));
+      W2 y{0u, 0u};
+      bool on = true;
+      if (w_is_zero(rhs.c1)) {  // rhs in Fp: the lane form
+        Fp2 yl;
+        on = fp2_sqrt_lane_i(yl, w2_to_fp2(rhs));
+        y = w2_from_fp2(yl);
+      } else {
+        const uint32_t nrm = wadd(wsqr(rhs.c0), wsqr(rhs.c1));
+        const uint32_t nr = wpow(nrm, EXP_SQRT, EXP_SQRT_BITS);
+        on = w_eq(K1, wsqr(nr), nrm);
+        const uint32_t inv2 = w_from_fp(FP_INV2);
+        const uint32_t t = wmul(wadd(rhs.c0, nr), inv2);
+        const uint32_t sr = wpow(t, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+        const uint32_t ts = wmul(t, sr), hs = wmul(wmul(rhs.c1, inv2), sr);
+        const bool tsq = w_is_one(wmul(ts, sr));
+        const uint32_t nts = wneg(K1, ts);
+        y = w2red(K, W2{tsq ? ts : hs, tsq ? hs : nts});
+      }
+      if (on) {
+        const Fp2 yl = w2_to_fp2(y);
+        if (fp2_lex_largest(yl) != a_flag) y = w2neg(K1, y);
+        y = w2red(K, y);
+        bool exc = false;
+        const J2W M = j2w_mul_xabs(K, J2W{xm, y, W2{K.one, 0u}}, exc);
+        // psi(sigma) == -M:  conj(x) CX Z^2 == X,  conj(y) CY Z^3 == -Y,  Z != 0
+        const W2 zz = w2mulk(K, M.z, M.z);
+        const W2 px = w2mulk(K, w2mulk(K, w2conj(K1, xm), w2const(PSI_CX)), zz);
+        const W2 py = w2mulk(K, w2mulk(K, w2conj(K1, y), w2const(PSI_CY)), w2mulk(K, zz, M.z));
+        const bool zx = w2_is_zero(w2subk(K.k2048_2, px, M.x));  // M.x < 1028p (the chain ends on a doubling)
+        const bool zy = w2_is_zero(w2add(py, M.y));
+        const bool zz0 = w2_is_zero(M.z);
+        if (!exc && !zz0 && zx && zy) {
+          v = 1;
+          s = G2A{w2_to_fp2(xm), w2_to_fp2(y), false};
+        }
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    out[i] = s;
+    ok[i] = v;
+  }
+}
+
+hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_validate_wide, dim3((unsigned)n), dim3(64), 0, st, sigs, n, out, ok);
+  return hipGetLastError();
+}
+
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad) {
   if (!nw) return hipSuccess;
   hipLaunchKernelGGL(k_wide_selftest, dim3((unsigned)nw), dim3(64), 0, st, nw, be48, bad);

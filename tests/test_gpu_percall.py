@@ -71,3 +71,24 @@ def test_percall_verify_message_lengths(mlen):
     avpks = [OC.SkToPk(k) for k in (21, 22, 23)]
     assert M.AggregateVerify(avpks, msgs, av) is True
     assert M.AggregateVerify(avpks, [msgs[1], msgs[0], msgs[2]], av) is False
+
+
+def test_percall_signature_edge_cases():
+    """The one-wave signature check of the per-call path on the signature edge cases: identity, bad flags, x >= p,
+    not on the curve, outside G2 (points of order 13 and 23 from the batch tests' construction are covered there),
+    and both y signs, against the C oracle's Verify."""
+    from bls_mi355x.backend import mi355x_bls as M
+    from oracle import bls_oracle_c as OC
+
+    msg = b"\x42" * 32
+    pk = OC.SkToPk(77)
+    sig = OC.Sign(77, msg)
+    cases = [sig, b"\xc0" + bytes(95), bytes(96), b"\x80" + bytes(95), b"\xe0" + bytes(95),
+             sig[:1] + b"\xff" * 47 + sig[48:], bytes([sig[0] ^ 0x20]) + sig[1:], sig[:95] + bytes([sig[95] ^ 1]),
+             b"\x9a\x01\x11\xea\x39\x7f\xe6\x9a\x4b\x1b\xa7\xb6\x43\x4b\xac\xd7\x64\x77\x4b\x84\xf3\x85\x12\xbf\x67"
+             b"\x30\xd2\xa0\xf6\xb0\xf6\x24\x1e\xab\xff\xfe\xb1\x53\xff\xff\xb9\xfe\xff\xff\xff\xff\xaa\xab" + bytes(48)]
+    for k in range(1, 6):  # both signs of several valid points (other messages: the verdict is False)
+        s = OC.Sign(k, msg)
+        cases += [s, bytes([s[0] ^ 0x20]) + s[1:]]
+    for c in cases:
+        assert M.Verify(pk, msg, c) == OC.Verify(pk, msg, c), c.hex()
