@@ -171,6 +171,15 @@ int d2h(bls_ctx* ctx, void* h, const void* d, size_t n) {
     if (e_ != hipSuccess) return fail(ctx, e_, #x);             \
   } while (0)
 
+constexpr size_t WIDE_H2C_MAX = 512;  // AggregateVerify: one wave per message up to this many
+constexpr size_t WIDE_KEYS_MAX = 4096;  // KeyValidate of a call's keys: two keys per wave up to this many
+
+// a call's keys (per-call FastAggregateVerify, AggregateVerify, AggregatePKs): the wide kernel's latency for a few
+// thousand keys, the lane kernel's throughput beyond (registry loads always take the lane kernel)
+static hipError_t launch_keys(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok) {
+  return n <= WIDE_KEYS_MAX ? launch_key_validate_wide(st, pks, n, out, ok) : launch_key_validate(st, pks, n, out, ok);
+}
+
 // Copy n compressed keys, validate them on the device; returns 1 if all valid.
 int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** outOk) {
   uint8_t* d_in;
@@ -180,7 +189,7 @@ int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** o
   SCR(S_G1A, n + 1, d_a);
   SCR(S_OK, n + 1, d_ok);
   CK(h2d(ctx, d_in, pks, 48 * n));
-  LK(launch_key_validate(ctx->j->stream, d_in, n, d_a, d_ok));
+  LK(launch_keys(ctx->j->stream, d_in, n, d_a, d_ok));
   std::vector<int> ok(n);
   CK(d2h(ctx, ok.data(), d_ok, n * sizeof(int)));
   *outA = d_a;
@@ -427,8 +436,6 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
 // exponentiation check.  Every chain that can be spread over a workgroup is
 // (the h2c and pairing phases); only the square roots and subgroup checks run
 // one lane each.
-constexpr size_t WIDE_H2C_MAX = 512;  // AggregateVerify: one wave per message up to this many
-
 static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
                           const uint8_t* sig96) {
   Job& J = *ctx->j;
@@ -479,7 +486,7 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   LK(hipGetLastError());
   LK(launch_miller_wave(st3, P + 2, Q + 1, ok + n, 1, f + 1));  // a rejected signature gives f = 1; `live` decides
   HIPCK(hipEventRecord(J.ev_msm, st3));
-  LK(launch_key_validate(st, d_pk, n, keys, ok));
+  LK(launch_keys(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));

@@ -95,5 +95,7 @@ hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, 
 hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag);
 // signature decode + subgroup check with one wave per signature (k_sig_validate semantics)
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
+// KeyValidate with two keys per wave (k_key_validate semantics)
+hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok);
 
 }  // namespace bls

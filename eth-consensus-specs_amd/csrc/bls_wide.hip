@@ -192,6 +192,114 @@ hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t 
   return hipGetLastError();
 }
 
+// ---- G1: KeyValidate with two keys per wave (one per half) ------------------
+// bls_fq_g1.h g1q_add_aff / g1q_add / g1q_dbl (complete projective, a = 0, 3b = 12) with the same subtraction
+// constants (64p, 128p) and the same value bounds (accumulator X < 66p, Y, Z < 4p; products below 2.0001p).
+struct G1W {
+  uint32_t x, y, z;
+};
+__device__ __forceinline__ G1W g1w_add_aff(const WKG& K, const G1W& p, uint32_t x2, uint32_t y2) {
+  const uint32_t t0 = wmul(p.x, x2);
+  const uint32_t t1 = wmul(p.y, y2);
+  const uint32_t t3 = wsubk(K.k2, wmul(wadd(x2, y2), wadd(p.x, p.y)), wadd(t0, t1));
+  const uint32_t t4 = wadd(wmul(y2, p.z), p.y);
+  const uint32_t y3 = wmuls<12>(wadd(wmul(x2, p.z), p.x));
+  const uint32_t t0p = wmuls<3>(t0);
+  const uint32_t t2 = wmuls<12>(p.z);
+  const uint32_t z3 = wadd(t1, t2);
+  const uint32_t t1p = wsubk(K.k1, t1, t2);
+  G1W r;
+  r.x = wsubk(K.k1, wmul(t3, t1p), wmul(t4, y3));
+  r.y = wadd(wmul(t1p, z3), wmul(y3, t0p));
+  r.z = wadd(wmul(z3, t4), wmul(t0p, t3));
+  return r;
+}
+__device__ __forceinline__ G1W g1w_add(const WKG& K, const G1W& p, const G1W& q) {
+  const uint32_t t0 = wmul(p.x, q.x), t1 = wmul(p.y, q.y), t2 = wmul(p.z, q.z);
+  const uint32_t t3 = wsubk(K.k2, wmul(wadd(p.x, p.y), wadd(q.x, q.y)), wadd(t0, t1));
+  const uint32_t t4 = wsubk(K.k2, wmul(wadd(p.y, p.z), wadd(q.y, q.z)), wadd(t1, t2));
+  const uint32_t y3 = wmuls<12>(wsubk(K.k2, wmul(wadd(p.x, p.z), wadd(q.x, q.z)), wadd(t0, t2)));
+  const uint32_t t0p = wmuls<3>(t0);
+  const uint32_t t2p = wmuls<12>(t2);
+  const uint32_t z3 = wadd(t1, t2p);
+  const uint32_t t1p = wsubk(K.k1, t1, t2p);
+  G1W r;
+  r.x = wsubk(K.k1, wmul(t3, t1p), wmul(t4, y3));
+  r.y = wadd(wmul(t1p, z3), wmul(y3, t0p));
+  r.z = wadd(wmul(z3, t4), wmul(t0p, t3));
+  return r;
+}
+__device__ __forceinline__ G1W g1w_dbl(const WKG& K, const G1W& p) {
+  const uint32_t t0 = wmul(p.y, p.y);
+  const uint32_t t1 = wmul(p.y, p.z);
+  const uint32_t t2 = wmuls<12>(wmul(p.z, p.z));  // 3b Z^2, < 24p
+  const uint32_t u = wmul(p.x, p.y);
+  const uint32_t z8 = wmuls<8>(t0);
+  const uint32_t x3a = wmul(t2, z8);
+  G1W r;
+  r.z = wmul(t1, z8);
+  const uint32_t w = wsubk(K.k2, t0, wmuls<3>(t2));  // t0 - 3 t2 + 128p
+  r.y = wadd(wmul(w, wadd(t0, t2)), x3a);
+  r.x = wmuls<2>(wmul(w, u));
+  return r;
+}
+template <bool AFF>
+__device__ __forceinline__ G1W g1w_mul_xabs(const WKG& K, const G1W& b) {
+  G1W m = b;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    m = g1w_dbl(K, m);
+    if ((X_ABS >> i) & 1ull) m = AFF ? g1w_add_aff(K, m, b.x, b.y) : g1w_add(K, m, b);
+  }
+  return m;
+}
+
+// KeyValidate of keys 2 blockIdx.x + half (k_key_validate semantics; the decode on every lane of the half, the
+// square root and both [|x|] chains in wide arithmetic).  Wave-uniform control flow: the two halves' decode
+// verdicts are combined into selects, not branches.
+__global__ void __launch_bounds__(64) k_key_validate_wide(const uint8_t* pks48, size_t n, G1A* out, int* ok) {
+  const size_t base = 2 * (size_t)blockIdx.x;
+  if (base >= n) return;
+  const WKG K = wkg_init();
+  const WK K1 = wk_of(K);
+  const int h = whalf();
+  const size_t i = base + (size_t)h < n ? base + (size_t)h : base;  // an odd tail: half 1 repeats key base
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(pks48 + 48 * i);
+  Fp x;
+#pragma unroll
+  for (int k = 0; k < 12; k++) x.l[11 - k] = __builtin_bswap32(w[k]);
+  const uint32_t flags = x.l[11] >> 24;
+  const bool c_flag = flags & 0x80, b_flag = flags & 0x40, a_flag = flags & 0x20;
+  x.l[11] &= 0x1fffffffu;
+  const bool fmt = c_flag && !b_flag && !fp_is_zero(x) && raw_lt_p(x);
+  const Fp xc = fp_mul_i(fmt ? x : FP_ONE, FP_R2);  // a malformed key runs the chain on a dummy, then fails
+  const uint32_t xm = w_from_fp(xc);
+  const uint32_t rhs = wadd(wmul(wsqr(xm), xm), w_from_fp(FP_B1));
+  const uint32_t y0 = wpow(rhs, EXP_SQRT, EXP_SQRT_BITS);
+  const bool on = w_eq(K1, wsqr(y0), rhs);
+  const uint32_t yr = wmul(y0, K.one);  // below 2.0001p
+  const Fp yl = w_to_fp(yr);
+  const bool flip = raw_gt_half(fp_from_mont(yl)) != a_flag;
+  const uint32_t ny = wmul(wneg(K1, yr), K.one);
+  const uint32_t y = flip ? ny : yr;
+  const G1W P{xm, y, K.one};
+  const G1W Q = g1w_mul_xabs<false>(K, g1w_mul_xabs<true>(K, P));
+  const bool eq_x = w_eq(K1, wmul(wmul(xm, w_from_fp(FP_BETA)), Q.z), wmul(Q.x, K.one));
+  const bool eq_y = w_is_zero(wadd(wmul(y, Q.z), Q.y));
+  const bool v = fmt && on && eq_x && eq_y;
+  const G1A a = v ? G1A{w_to_fp(xm), w_to_fp(y), false} : G1A{fp_zero(), fp_zero(), true};
+  if (wpos() == 0 && base + (size_t)h < n) {
+    out[base + h] = a;
+    ok[base + h] = v ? 1 : 0;
+  }
+}
+
+hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_key_validate_wide, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, pks, n, out, ok);
+  return hipGetLastError();
+}
+
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad) {
   if (!nw) return hipSuccess;
   hipLaunchKernelGGL(k_wide_selftest, dim3((unsigned)nw), dim3(64), 0, st, nw, be48, bad);

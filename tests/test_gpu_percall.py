@@ -92,3 +92,24 @@ def test_percall_signature_edge_cases():
         cases += [s, bytes([s[0] ^ 0x20]) + s[1:]]
     for c in cases:
         assert M.Verify(pk, msg, c) == OC.Verify(pk, msg, c), c.hex()
+
+
+def test_wide_key_validate_edge_cases():
+    """KeyValidate through the two-keys-per-wave kernel (per-call keys, AggregatePKs, AggregateVerify) on small x
+    (on-curve points almost all outside G1, off-curve x, both sign bits), valid keys and the fixtures' malformed
+    encodings, against the C oracle; and a 515-key AggregatePKs (odd count: the last wave's second half idles)."""
+    from bls_mi355x.backend import mi355x_bls as M
+    from oracle import bls_oracle_c as OC
+
+    keys = []
+    for x in range(1, 24):
+        for flag in (0x80, 0xA0):
+            b = bytearray(x.to_bytes(48, "big"))
+            b[0] |= flag
+            keys.append(bytes(b))
+    keys += [OC.SkToPk(k) for k in (1, 2, 3, 0xDEADBEEF)]
+    keys += [b"\xc0" + bytes(47), b"\x40" + bytes(47), bytes(48), b"\x80" + bytes(47)]
+    for pk in keys:
+        assert M.KeyValidate(pk) == OC.KeyValidate(pk), pk.hex()
+    pks = [OC.SkToPk(k) for k in range(1, 516)]
+    assert M.AggregatePKs(pks) == OC.AggregatePKs(pks)
