@@ -111,6 +111,7 @@ _SIGS = {
     "bls_test_hash_to_g2_batch": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_test_wide_selftest": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_test_hash_to_g2_wide": (_ip, [_vp, _u8p, _sz, _vp]),
+    "bls_test_h2c_wide_stages": (_ip, [_vp, _u8p, _vp]),
 }
 
 EXPORTS = tuple(_SIGS)

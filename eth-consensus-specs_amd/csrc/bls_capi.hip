@@ -771,6 +771,20 @@ int bls_test_hash_to_g2_wide(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint
   return 0;
 }
 
+// stages of the one-wave hash for one 32-byte message (k_h2c_wide_dbg): 33 x 48-byte little-endian raw Fp
+int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out) {
+  API_ENTER(ctx);
+  if (!msg32 || !out) return BLS_E_ARG;
+  uint8_t* d_m;
+  Fp* d_out;
+  SCR(S_IN0, 32, d_m);
+  SCR(S_G2A, 20, d_out);
+  CK(h2d(ctx, d_m, msg32, 32));
+  LK(launch_h2c_wide_dbg(ctx->j->stream, d_m, d_out));
+  CK(d2h(ctx, out, d_out, 33 * sizeof(Fp)));
+  return 0;
+}
+
 int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96) {
   API_ENTER(ctx);
   if ((!msgs32 || !out96) && n) return BLS_E_ARG;

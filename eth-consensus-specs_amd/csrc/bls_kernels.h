@@ -93,6 +93,7 @@ hipError_t launch_gt_mul(hipStream_t st, const uint8_t* a, const uint8_t* b, uin
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad);
 // hash_to_G2 with one wave per message (msgs 32 B apart when offs is null); flag[i] = 1: recompute on the fallback
 hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag);
+hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out);
 // signature decode + subgroup check with one wave per signature (k_sig_validate semantics)
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
 // KeyValidate with two keys per wave (k_key_validate semantics)

@@ -105,6 +105,75 @@ __global__ void __launch_bounds__(64) k_h2c_wide(size_t B, const uint8_t* msgs, 
   }
 }
 
+// Debug view of k_h2c_wide for one 32-byte message (tests): out[] = raw (non-Montgomery) little-endian Fp limbs of,
+// per half h: u_h (2), SSWU x (2), y (2), the isogeny's Jacobian point as affine x, y (4); then Q = P0 + P1 affine
+// (4), M = [|x|] Q affine (4), H affine (4), and the flags (rare, izero, exc) of both halves as one Fp word.
+__device__ __forceinline__ void dbg_put(Fp* out, int k, const Fp& v) {
+  if (threadIdx.x == 0) out[k] = fp_from_mont(v);
+}
+__global__ void __launch_bounds__(64) k_h2c_wide_dbg(const uint8_t* msg32, Fp* out) {
+  const WKG K = wkg_init();
+  Fp2 u[2];
+  hash_to_field_fp2_m32(u, msg32);
+  const bool hi = whalf() != 0;
+  const Fp2 uh{fp_select(hi, u[1].c0, u[0].c0), fp_select(hi, u[1].c1, u[0].c1)};
+  W2 x, y;
+  bool rare = false, izero = false, exc = false;
+  sswu_w(K, uh, x, y, rare);
+  const J2W P = iso_w(K, x, y, izero);
+  const G2A pa = j2w_to_aff(K, P);
+  for (int h = 0; h < 2; h++) {
+    // lane 0 writes; values of half h read through w_to_fp from lane 32 h: take them from the lane's own half
+    const Fp2 xs = w2_to_fp2(x), ys = w2_to_fp2(y);
+    const Fp v[10] = {uh.c0, uh.c1, xs.c0, xs.c1, ys.c0, ys.c1, pa.x.c0, pa.x.c1, pa.y.c0, pa.y.c1};
+    for (int k = 0; k < 10; k++) {
+      const Fp vk = v[k];
+      Fp o;
+#pragma unroll
+      for (int l = 0; l < 12; l++) o.l[l] = (uint32_t)__builtin_amdgcn_readlane((int)vk.l[l], 32 * h);
+      dbg_put(out, 10 * h + k, o);
+    }
+  }
+  const J2W Po{w2swap(P.x), w2swap(P.y), w2swap(P.z)};
+  const J2W Q = j2w_add(K, P, Po, exc);
+  const G2A qa = j2w_to_aff(K, Q);
+  dbg_put(out, 20, qa.x.c0);
+  dbg_put(out, 21, qa.x.c1);
+  dbg_put(out, 22, qa.y.c0);
+  dbg_put(out, 23, qa.y.c1);
+  const J2W M = j2w_mul_xabs(K, Q, exc);
+  const G2A ma = j2w_to_aff(K, M);
+  dbg_put(out, 24, ma.x.c0);
+  dbg_put(out, 25, ma.x.c1);
+  dbg_put(out, 26, ma.y.c0);
+  dbg_put(out, 27, ma.y.c1);
+  const W2 cx = w2const(PSI_CX), cy = w2const(PSI_CY);
+  const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
+  const J2W npq = j2w_neg(K, j2w_psi(K, Q, cx, cy));
+  const J2W Ap = j2w_add(K, M, npq, exc);
+  J2W C = j2w_add(K, j2w_psi2(K, j2w_dbl(K, Q), c2x, c2y), npq, exc);
+  C = j2w_add(K, C, M, exc);
+  C = j2w_add(K, C, j2w_neg(K, Q), exc);
+  const J2W M2 = j2w_mul_xabs(K, Ap, exc);
+  const G2A h = j2w_to_aff(K, j2w_add(K, C, M2, exc));
+  dbg_put(out, 28, h.x.c0);
+  dbg_put(out, 29, h.x.c1);
+  dbg_put(out, 30, h.y.c0);
+  dbg_put(out, 31, h.y.c1);
+  const int fl = (rare ? 1 : 0) | (izero ? 2 : 0) | (exc ? 4 : 0);
+  const int f0 = __builtin_amdgcn_readlane(fl, 0), f1 = __builtin_amdgcn_readlane(fl, 32);
+  if (threadIdx.x == 0) {
+    Fp o = fp_zero();
+    o.l[0] = (uint32_t)(f0 | (f1 << 8));
+    out[32] = o;
+  }
+}
+
+hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out) {
+  hipLaunchKernelGGL(k_h2c_wide_dbg, dim3(1), dim3(64), 0, st, msg32, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag) {
   if (!B) return hipSuccess;
   hipLaunchKernelGGL(k_h2c_wide, dim3((unsigned)B), dim3(64), 0, st, B, msgs, offs, H, flag);

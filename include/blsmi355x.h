@@ -285,6 +285,8 @@ int bls_test_force_h2c_fallback(bls_ctx* ctx, const uint8_t* mask, size_t n);
 int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96);
 /* the same through the one-wave-per-message kernel of the per-call path */
 int bls_test_hash_to_g2_wide(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96);
+/* intermediate stages of the one-wave hash of one 32-byte message (debugging) */
+int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out);
 /* bls_test_wide_selftest: nw waves compare the wavefront-cooperative products
  * (bls_wide.h) with the lane form on four inputs each (48-byte big-endian
  * integers < p); bad[w] = bitmask of differing forms, 0 when all agree. */

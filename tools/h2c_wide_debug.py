@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Stage-by-stage comparison of the one-wave hash_to_G2 (bls_test_h2c_wide_stages) with the Python oracle."""
+import ctypes
+import hashlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "eth-consensus-specs_amd")):
+    sys.path.insert(0, p)
+from bls_mi355x import _native  # noqa: E402
+from oracle import bls_oracle as O  # noqa: E402
+
+DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+
+
+def main():
+    ctx = _native.context()
+    for j in range(int(os.environ.get("N", "3"))):
+        msg = hashlib.sha256(b"wide" + j.to_bytes(4, "little")).digest()
+        buf = ctypes.create_string_buffer(33 * 48)
+        ctx.check(ctx.lib.bls_test_h2c_wide_stages(ctx.h, msg, buf))
+        v = [int.from_bytes(buf.raw[48 * k: 48 * k + 48], "little") for k in range(33)]
+        u = O.hash_to_field_fp2(msg, 2, DST)
+        res = {}
+        for h in range(2):
+            b = 10 * h
+            res[f"u{h}"] = (v[b], v[b + 1]) == u[h]
+            xy = O.map_to_curve_sswu(u[h])
+            res[f"sswu{h}"] = ((v[b + 2], v[b + 3]), (v[b + 4], v[b + 5])) == xy
+            iso = O.iso_map(xy)
+            res[f"iso{h}"] = ((v[b + 6], v[b + 7]), (v[b + 8], v[b + 9])) == (iso[0], iso[1])
+        q = O.g2_add(O.iso_map(O.map_to_curve_sswu(u[0])), O.iso_map(O.map_to_curve_sswu(u[1])))
+        res["Q"] = ((v[20], v[21]), (v[22], v[23])) == (q[0], q[1])
+        m = O.g2_mul(q, 0xD201000000010000)
+        res["M"] = ((v[24], v[25]), (v[26], v[27])) == (m[0], m[1])
+        hh = O.clear_cofactor_g2(q)
+        res["H"] = ((v[28], v[29]), (v[30], v[31])) == (hh[0], hh[1])
+        res["flags"] = hex(v[32])
+        print(j, res, flush=True)
+        if not res["sswu0"]:
+            print("  sswu0 got", hex(v[2])[:20], "want", hex(O.map_to_curve_sswu(u[0])[0][0])[:20])
+
+
+if __name__ == "__main__":
+    main()
