@@ -35,7 +35,7 @@ enum Slot {
   S_PT_IN, S_PT_A, S_PT_OK, S_PT_TMP, S_PT_OUT,
   // per-call Verify / FastAggregateVerify pair points (not S_RP: a FAV batch's r_i apk_i live there between its
   // partial and finish calls, and fav_bisect reads them back)
-  S_PC_P,
+  S_PC_P, S_PC_L,
   NSLOT
 };
 
@@ -461,6 +461,8 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_AV_HCF, h2c_scratch_fd(1), hf);
   SCR(S_AV_FLAG, 1, flag);
   SCR(S_F, 3, f);  // f(apk, H) | f(-G1, sigma) | their product
+  uint32_t* L;
+  SCR(S_PC_L, lines_wide_u32(2), L);  // line records of the two pairs (F2 layout)
   SCR(S_INT, 4, d_r);
   uint8_t* d_pk = d_in;
   uint8_t* d_sig = d_in + 48 * n;
@@ -484,16 +486,17 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipEventRecord(J.ev_sig, st3));
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, P + 2);
   LK(hipGetLastError());
-  LK(launch_miller_wave(st3, P + 2, Q + 1, ok + n, 1, f + 1));  // a rejected signature gives f = 1; `live` decides
+  // the G2 side of the Miller loop of (-G1, sigma) while hash_to_G2 runs (a rejected signature: constant lines)
+  LK(launch_lines_wide(st3, P + 2, Q + 1, ok + n, 1, L + lines_wide_u32(1)));
   HIPCK(hipEventRecord(J.ev_msm, st3));
   LK(launch_keys(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
-  LK(launch_miller_wave(st, P, Q, nullptr, 1, f));  // rejected inputs are identities here; `live` decides
+  LK(launch_lines_wide(st, P, Q, nullptr, 1, L));  // rejected inputs are identities here; `live` decides
   HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
-  LK(launch_fp12_chunk_prod(st, f, 2, 2, f + 2));
+  LK(launch_facc_wide(st, L, 2, f + 2));  // f(apk, H) f(-G1, sigma), one shared squaring per step
   int live = 0;
   HIPCK(hipMemcpyAsync(&live, ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
   const int fe = run_final_check(ctx, f + 2);  // orders after st
@@ -778,10 +781,10 @@ int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out) {
   uint8_t* d_m;
   Fp* d_out;
   SCR(S_IN0, 32, d_m);
-  SCR(S_G2A, 20, d_out);
+  SCR(S_G2A, 45, d_out);
   CK(h2d(ctx, d_m, msg32, 32));
   LK(launch_h2c_wide_dbg(ctx->j->stream, d_m, d_out));
-  CK(d2h(ctx, out, d_out, 33 * sizeof(Fp)));
+  CK(d2h(ctx, out, d_out, 45 * sizeof(Fp)));
   return 0;
 }
 

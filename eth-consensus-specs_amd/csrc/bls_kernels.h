@@ -96,6 +96,11 @@ hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const 
 hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out);
 // signature decode + subgroup check with one wave per signature (k_sig_validate semantics)
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
+// Miller loop in F2 layout: the line records of n pairs (one wave each), then f over npairs pairs' lines (one
+// workgroup of six waves; conjugated, tower layout)
+hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L);
+hipError_t launch_facc_wide(hipStream_t st, const uint32_t* L, int npairs, Fp12* out);
+size_t lines_wide_u32(size_t n);
 // KeyValidate with two keys per wave (k_key_validate semantics)
 hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok);
 

@@ -263,5 +263,51 @@ __device__ __forceinline__ bool w2_is_zero(W2 a) { return w_is_zero(a.c0) && w_i
 __device__ __forceinline__ W2 w2swap(W2 a) { return W2{wswap(a.c0), wswap(a.c1)}; }
 __device__ __forceinline__ W2 w2sel(bool c, W2 a, W2 b) { return W2{c ? a.c0 : b.c0, c ? a.c1 : b.c1}; }
 
+// ---- Fp2 in F2 layout: one VGPR, c0 in half 0 and c1 in half 1 (D layout each) ----
+// An Fp2 product is ONE wdot2 per half (both halves at once): half 0 forms c0 = a0 b0 + a1 (kn - b1), half 1
+// c1 = a0 b1 + a1 b0, each reading the other half's coefficients through one ds_bpermute (wswap).  kn is a
+// multiple of p in borrowed digits covering b1 (the 4096p of bls_fq_g2.h for b1 < 4096p).
+__device__ __forceinline__ uint32_t wf_mul(uint32_t kn, uint32_t a, uint32_t b) {
+  const bool h = whalf() != 0;
+  const uint32_t sa = wswap(a), sb = wswap(b);
+  const uint32_t nb1 = wnorm(kn - sb);
+  return wdot2(h ? sa : a, b, h ? a : sa, h ? sb : nb1);
+}
+// (a0 + a1)(a0 - a1 + ks) in half 0, a0 (2 a1) in half 1 (ks covering a1)
+__device__ __forceinline__ uint32_t wf_sqr(uint32_t ks, uint32_t a) {
+  const bool h = whalf() != 0;
+  const uint32_t sa = wswap(a);
+  const uint32_t x = h ? sa : wadd(a, sa);
+  const uint32_t y = h ? wmuls<2>(a) : wnorm(a + (ks - sa));
+  return wmul(x, y);
+}
+// a xi = (a0 - a1) + (a0 + a1) u  (k covering a1)
+__device__ __forceinline__ uint32_t wf_xi(uint32_t k, uint32_t a) {
+  const bool h = whalf() != 0;
+  const uint32_t sa = wswap(a);
+  const uint32_t d = wnorm(a + (k - sa)), s = wadd(a, sa);
+  return h ? s : d;
+}
+// conj(a) (k covering a1)
+__device__ __forceinline__ uint32_t wf_conj(uint32_t k, uint32_t a) {
+  const uint32_t n = wnorm(k - a);
+  return whalf() ? n : a;
+}
+// an Fp2 constant / lane-local Fp2 value in F2 layout
+__device__ __forceinline__ uint32_t wf_from_fp2(const Fp2& a) {
+  const bool h = whalf() != 0;
+  return w_from_fq(fq_unpack(h ? a.c1 : a.c0));
+}
+// canonical packed Fp2 on every lane
+__device__ __forceinline__ Fp2 wf_to_fp2(uint32_t v) {
+  Fq c0, c1;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    c0.d[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+    c1.d[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, 32 + i);
+  }
+  return Fp2{fq_pack(c0), fq_pack(c1)};
+}
+
 }  // namespace wide
 }  // namespace bls

@@ -5,6 +5,7 @@
 #include "bls_lane.h"
 #include "bls_wide.h"
 #include "bls_wide_g2.h"
+#include "bls_pp_lane.h"
 #include "bls_xmd32.h"
 #include "bls_h2c.h"
 
@@ -137,6 +138,75 @@ __global__ void __launch_bounds__(64) k_h2c_wide_dbg(const uint8_t* msg32, Fp* o
   const J2W Po{w2swap(P.x), w2swap(P.y), w2swap(P.z)};
   const J2W Q = j2w_add(K, P, Po, exc);
   const G2A qa = j2w_to_aff(K, Q);
+  {  // the lane form on the same inputs, and the first intermediates of both forms (slots 33 ..)
+    const G2J pl{w2_to_fp2(P.x), w2_to_fp2(P.y), w2_to_fp2(P.z)}, ql{w2_to_fp2(Po.x), w2_to_fp2(Po.y), w2_to_fp2(Po.z)};
+    bool e2 = false;
+    const G2J rl = j2_add(pl, ql, e2);
+    const G2A ra = jac_to_aff(rl);
+    dbg_put(out, 33, ra.x.c0);
+    dbg_put(out, 34, ra.x.c1);
+    dbg_put(out, 35, ra.y.c0);
+    dbg_put(out, 36, ra.y.c1);
+    {  // every intermediate of j2w_add against j2_add's, as a bit mask in slot 32's high word
+      const J2W& wp = P;
+      const J2W& wq = Po;
+      const WK K1 = wk_of(K);
+      (void)K1;
+      int bm = 0, bit = 0;
+      auto chk = [&](const W2& a, const Fp2& b) { if (!fp2_eq(w2_to_fp2(a), b)) bm |= 1 << bit; bit++; };
+      const W2 Z1 = w2sqrk(K, wp.z), Z2 = w2sqrk(K, wq.z);
+      const Fp2 z1 = f2sqr(pl.z), z2 = f2sqr(ql.z);
+      chk(Z1, z1); chk(Z2, z2);
+      const W2 U1 = w2mulk(K, wp.x, Z2), U2 = w2mulk(K, wq.x, Z1);
+      const Fp2 u1x = f2mul(pl.x, z2), u2x = f2mul(ql.x, z1);
+      chk(U1, u1x); chk(U2, u2x);
+      const W2 S1 = w2mulk(K, w2mulk(K, wp.y, wq.z), Z2), S2 = w2mulk(K, w2mulk(K, wq.y, wp.z), Z1);
+      const Fp2 s1 = f2mul(f2mul(pl.y, ql.z), z2), s2 = f2mul(f2mul(ql.y, pl.z), z1);
+      chk(S1, s1); chk(S2, s2);
+      const W2 H = w2subk(K.k256, U2, U1);
+      const Fp2 hh = fp2_sub(u2x, u1x);
+      chk(H, hh);
+      const W2 RR = w2muls<2>(w2subk(K.k256, S2, S1));
+      const Fp2 rr = fp2_dbl(fp2_sub(s2, s1));
+      chk(RR, rr);
+      const W2 I = w2sqrk(K, w2muls<2>(H));
+      const Fp2 ii = f2sqr(fp2_dbl(hh));
+      chk(I, ii);
+      const W2 J = w2mulk(K, H, I), V = w2mulk(K, U1, I);
+      const Fp2 jj = f2mul(hh, ii), vv = f2mul(u1x, ii);
+      chk(J, jj); chk(V, vv);
+      const W2 RRS = w2sqrk(K, RR);
+      chk(RRS, f2sqr(rr));
+      const W2 X3 = w2subk(K.k512_2, RRS, w2add(J, w2muls<2>(V)));
+      const Fp2 x3 = fp2_sub(fp2_sub(f2sqr(rr), jj), fp2_dbl(vv));
+      chk(X3, x3);
+      const W2 VX = w2subk(K.k1024, V, X3);
+      chk(VX, fp2_sub(vv, x3));
+      const W2 Y3 = w2subk(K.k512_2, w2mulk(K, RR, VX), w2muls<2>(w2mulk(K, S1, J)));
+      chk(Y3, fp2_sub(f2mul(rr, fp2_sub(vv, x3)), fp2_dbl(f2mul(s1, jj))));
+      const W2 ZZ = w2subk(K.k2, w2sqrk(K, w2add(wp.z, wq.z)), w2add(Z1, Z2));
+      chk(ZZ, fp2_sub(fp2_sub(f2sqr(fp2_add(pl.z, ql.z)), z1), z2));
+      const int b0 = __builtin_amdgcn_readlane(bm, 0);
+      if (threadIdx.x == 0) {
+        Fp o = fp_zero();
+        o.l[1] = (uint32_t)b0;
+        out[32] = o;
+      }
+    }
+    const W2 z1z1 = w2sqrk(K, P.z);
+    const Fp2 z1l = f2sqr(pl.z);
+    const W2 u1 = w2mulk(K, P.x, w2sqrk(K, Po.z));
+    const Fp2 u1l = f2mul(pl.x, f2sqr(ql.z));
+    const Fp2 zw = w2_to_fp2(z1z1), uw = w2_to_fp2(u1);
+    dbg_put(out, 37, zw.c0);
+    dbg_put(out, 38, zw.c1);
+    dbg_put(out, 39, z1l.c0);
+    dbg_put(out, 40, z1l.c1);
+    dbg_put(out, 41, uw.c0);
+    dbg_put(out, 42, uw.c1);
+    dbg_put(out, 43, u1l.c0);
+    dbg_put(out, 44, u1l.c1);
+  }
   dbg_put(out, 20, qa.x.c0);
   dbg_put(out, 21, qa.x.c1);
   dbg_put(out, 22, qa.y.c0);
@@ -162,11 +232,8 @@ __global__ void __launch_bounds__(64) k_h2c_wide_dbg(const uint8_t* msg32, Fp* o
   dbg_put(out, 31, h.y.c1);
   const int fl = (rare ? 1 : 0) | (izero ? 2 : 0) | (exc ? 4 : 0);
   const int f0 = __builtin_amdgcn_readlane(fl, 0), f1 = __builtin_amdgcn_readlane(fl, 32);
-  if (threadIdx.x == 0) {
-    Fp o = fp_zero();
-    o.l[0] = (uint32_t)(f0 | (f1 << 8));
-    out[32] = o;
-  }
+  __syncthreads();
+  if (threadIdx.x == 0) out[32].l[0] = (uint32_t)(f0 | (f1 << 8));
 }
 
 hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out) {
@@ -368,6 +435,159 @@ hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n
   hipLaunchKernelGGL(k_key_validate_wide, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, pks, n, out, ok);
   return hipGetLastError();
 }
+
+// ---- Miller loop in F2 layout (per-call path) ------------------------------
+// Split like the batch kernels: the G2 side (T and the line records) per pair, then the f accumulation shared by
+// the pairs.  Line record of a step: (l0, l2, l3) with the P factors applied (l2 = (E ZZ) (-x_P) or r (-x_P),
+// l3 = (z3 ZZ) y_P or z3 y_P; bls_pairing.h ml_dbl_step / ml_add_step), three Fp2 in F2 layout = 3 x 64 words.
+// A pair that is not live runs with P = (0, 0) and Q = the G2 generator: its lines are constants in Fp2, which
+// the final exponentiation maps to 1 (as k_miller2_vm).
+constexpr int MLW_STEPS = 68;  // 63 doublings + 5 additions
+
+// one wave per pair; every Fp2 in F2 layout, products one after another.  Value bounds (units of p; products
+// < 2.0001): doubling in X < 516, Y, Z < 66 -> X3 < 516, Y3, Z3 < 66; addition -> all < 66; lines l0 < 66,
+// l2 and l3 products.  Subtraction constants: 64p for products and small sums, 256p / 512p / 1024p where the
+// subtrahend is a coordinate; the Fp2 products negate with 4096p (kneg), squarings with 2048p.
+__global__ void __launch_bounds__(64) k_lines_wide(const G1A* P, const G2A* Q, const int* ok, size_t n,
+                                                   uint32_t* L) {
+  const size_t i = blockIdx.x;
+  if (i >= n) return;
+  const WKG K = wkg_init();
+  const int lane = wlane();
+  const bool live = (!ok || ok[i]) && !P[i].inf && !Q[i].inf;
+  const G2A q = live ? Q[i] : g2_generator();
+  const uint32_t nxP = live ? w_from_fp(fp_neg(P[i].x)) : 0u, yP = live ? w_from_fp(P[i].y) : 0u;
+  const uint32_t xQ = wf_from_fp2(q.x), yQ = wf_from_fp2(q.y);
+  uint32_t X = xQ, Y = yQ, Z = wf_from_fp2(fp2_one());
+  uint32_t* o = L + (size_t)i * MLW_STEPS * 3 * 64 + lane;
+  const uint32_t kn = K.kneg, ks = K.k2048_2;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    {  // doubling
+      const uint32_t A = wf_sqr(ks, X), B = wf_sqr(ks, Y), C = wf_sqr(ks, B);
+      const uint32_t XB = wf_sqr(ks, wadd(X, B));
+      const uint32_t D = wmuls<2>(wsubk(K.k1, XB, wadd(A, C)));
+      const uint32_t E = wmuls<3>(A);
+      const uint32_t F = wf_sqr(ks, E), ZZ = wf_sqr(ks, Z);
+      const uint32_t l0 = wsubk(K.k1, wf_mul(kn, E, X), wmuls<2>(B));
+      const uint32_t l2 = wmul(wf_mul(kn, E, ZZ), nxP);
+      const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Y, Z)), wadd(B, ZZ));
+      const uint32_t l3 = wmul(wf_mul(kn, z3, ZZ), yP);
+      const uint32_t x3 = wsubk(K.k512_2, F, wmuls<2>(D));
+      const uint32_t y3 = wsubk(K.k1, wf_mul(kn, E, wsubk(K.k1024, D, x3)), wmuls<8>(C));
+      X = x3;
+      Y = y3;
+      Z = z3;
+      o[0] = l0;
+      o[64] = l2;
+      o[128] = l3;
+      o += 3 * 64;
+    }
+    if ((X_ABS >> b) & 1ull) {  // addition of Q (affine)
+      const uint32_t z1z1 = wf_sqr(ks, Z);
+      const uint32_t u2 = wf_mul(kn, xQ, z1z1);
+      const uint32_t s2 = wf_mul(kn, wf_mul(kn, yQ, Z), z1z1);
+      const uint32_t h = wsubk(K.k1024, u2, X);
+      const uint32_t hh = wf_sqr(ks, h);
+      const uint32_t i4 = wmuls<4>(hh);
+      const uint32_t j = wf_mul(kn, h, i4);
+      const uint32_t r = wmuls<2>(wsubk(K.k256, s2, Y));
+      const uint32_t v = wf_mul(kn, X, i4);
+      const uint32_t x3 = wsubk(K.k1, wf_sqr(ks, r), wadd(j, wmuls<2>(v)));
+      const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, Y, j)));
+      const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Z, h)), wadd(z1z1, hh));
+      const uint32_t l0 = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
+      o[0] = l0;
+      o[64] = wmul(r, nxP);
+      o[128] = wmul(z3, yP);
+      o += 3 * 64;
+      X = x3;
+      Y = y3;
+      Z = z3;
+    }
+  }
+}
+
+// f accumulation: six waves, wave k owns the w^k coefficient of f (w-basis: w^6 = xi; w^2k is c0.c_k, w^(2k+1)
+// is c1.c_k of the tower).  f lives in LDS in F2 layout; a squaring or line product reads the operands of each of
+// the wave's products from LDS, so the per-wave term tables need no register indexing.
+//   f^2:  c_k = sum_{i+j=k} a_i a_j + xi sum_{i+j=k+6} a_i a_j   (3-4 products per wave)
+//   f l:  c_k = a_k l0 + a_{k-2} l2 + a_{k-3} l3  (indices mod 6, xi on wrap-around)   (3 products)
+// Values: f below ~100p (sums of <= 4 products and one xi), lines below 66p: every product operand pair is far
+// below p R, every xi argument (a sum of products, < 10.001p) below the 64p it is negated against.
+__constant__ uint8_t FSQ_TERMS[6][4][4] = {  // (i, j, multiplier, xi) ; multiplier 0 pads
+    {{0, 0, 1, 0}, {1, 5, 2, 1}, {2, 4, 2, 1}, {3, 3, 1, 1}},
+    {{0, 1, 2, 0}, {2, 5, 2, 1}, {3, 4, 2, 1}, {0, 0, 0, 0}},
+    {{0, 2, 2, 0}, {1, 1, 1, 0}, {3, 5, 2, 1}, {4, 4, 1, 1}},
+    {{0, 3, 2, 0}, {1, 2, 2, 0}, {4, 5, 2, 1}, {0, 0, 0, 0}},
+    {{0, 4, 2, 0}, {1, 3, 2, 0}, {2, 2, 1, 0}, {5, 5, 1, 1}},
+    {{0, 5, 2, 0}, {1, 4, 2, 0}, {2, 3, 2, 0}, {0, 0, 0, 0}}};
+
+__global__ void __launch_bounds__(384) k_facc_wide(const uint32_t* L, int npairs, Fp12* out) {
+  __shared__ uint32_t fs[6 * 64];
+  const WKG K = wkg_init();
+  const int lane = wlane(), k = (int)(threadIdx.x >> 6);
+  const uint32_t kn = K.kneg;
+  fs[k * 64 + lane] = k == 0 ? wf_from_fp2(fp2_one()) : 0u;
+  __syncthreads();
+  int step = 0;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) {  // f = f^2
+      uint32_t plain = 0, xs = 0;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const uint32_t ii = FSQ_TERMS[k][t][0], jj = FSQ_TERMS[k][t][1], m = FSQ_TERMS[k][t][2];
+        const uint32_t pr = wf_mul(kn, fs[ii * 64 + lane], fs[jj * 64 + lane]);
+        const uint32_t pm = wnorm(pr * m);
+        if (FSQ_TERMS[k][t][3]) xs = wadd(xs, pm); else plain = wadd(plain, pm);
+      }
+      const uint32_t c = wadd(plain, wf_xi(K.k1, xs));
+      __syncthreads();
+      fs[k * 64 + lane] = c;
+      __syncthreads();
+    }
+    const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
+#pragma unroll 1
+    for (int sl = 0; sl < nl; ++sl, ++step) {
+#pragma unroll 1
+      for (int pi = 0; pi < npairs; ++pi) {
+        const uint32_t* l = L + ((size_t)pi * MLW_STEPS + step) * 3 * 64 + lane;
+        const uint32_t l0 = l[0], l2 = l[64], l3 = l[128];
+        const int i2 = (k + 4) % 6, i3 = (k + 3) % 6;
+        const uint32_t p0 = wf_mul(kn, fs[k * 64 + lane], l0);
+        const uint32_t p2 = wf_mul(kn, fs[i2 * 64 + lane], l2);
+        const uint32_t p3 = wf_mul(kn, fs[i3 * 64 + lane], l3);
+        const uint32_t xw = wadd(k < 2 ? p2 : 0u, k < 3 ? p3 : 0u);
+        const uint32_t pl = wadd(p0, wadd(k < 2 ? 0u : p2, k < 3 ? 0u : p3));
+        const uint32_t c = wadd(pl, wf_xi(K.k1, xw));
+        __syncthreads();
+        fs[k * 64 + lane] = c;
+        __syncthreads();
+      }
+    }
+  }
+  // x < 0: conjugate (negate the odd w-coefficients); canonical Fp2 into the tower slot of w^k
+  const uint32_t c = fs[k * 64 + lane];
+  const uint32_t neg = (k & 1) ? wnorm(K.k1024 - c) : c;  // -c on both halves (c < 100p)
+  const Fp2 v = wf_to_fp2(neg);
+  if (lane == 0) {
+    Fp6& h6 = (k & 1) ? out->c1 : out->c0;
+    Fp2& dst = (k >> 1) == 0 ? h6.c0 : ((k >> 1) == 1 ? h6.c1 : h6.c2);
+    dst = v;
+  }
+}
+
+hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_lines_wide, dim3((unsigned)n), dim3(64), 0, st, P, Q, ok, n, L);
+  return hipGetLastError();
+}
+hipError_t launch_facc_wide(hipStream_t st, const uint32_t* L, int npairs, Fp12* out) {
+  hipLaunchKernelGGL(k_facc_wide, dim3(1), dim3(384), 0, st, L, npairs, out);
+  return hipGetLastError();
+}
+size_t lines_wide_u32(size_t n) { return n * (size_t)MLW_STEPS * 3 * 64; }
 
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad) {
   if (!nw) return hipSuccess;

@@ -18,9 +18,9 @@ def main():
     ctx = _native.context()
     for j in range(int(os.environ.get("N", "3"))):
         msg = hashlib.sha256(b"wide" + j.to_bytes(4, "little")).digest()
-        buf = ctypes.create_string_buffer(33 * 48)
+        buf = ctypes.create_string_buffer(45 * 48)
         ctx.check(ctx.lib.bls_test_h2c_wide_stages(ctx.h, msg, buf))
-        v = [int.from_bytes(buf.raw[48 * k: 48 * k + 48], "little") for k in range(33)]
+        v = [int.from_bytes(buf.raw[48 * k: 48 * k + 48], "little") for k in range(45)]
         u = O.hash_to_field_fp2(msg, 2, DST)
         res = {}
         for h in range(2):
@@ -37,6 +37,9 @@ def main():
         hh = O.clear_cofactor_g2(q)
         res["H"] = ((v[28], v[29]), (v[30], v[31])) == (hh[0], hh[1])
         res["flags"] = hex(v[32])
+        res["Q_lane"] = ((v[33], v[34]), (v[35], v[36])) == (q[0], q[1])
+        res["z1z1"] = (v[37], v[38]) == (v[39], v[40])
+        res["u1"] = (v[41], v[42]) == (v[43], v[44])
         print(j, res, flush=True)
         if not res["sswu0"]:
             print("  sswu0 got", hex(v[2])[:20], "want", hex(O.map_to_curve_sswu(u[0])[0][0])[:20])
