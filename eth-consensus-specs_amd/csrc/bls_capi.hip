@@ -781,10 +781,10 @@ int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out) {
   uint8_t* d_m;
   Fp* d_out;
   SCR(S_IN0, 32, d_m);
-  SCR(S_G2A, 45, d_out);
+  SCR(S_G2A, 100, d_out);
   CK(h2d(ctx, d_m, msg32, 32));
   LK(launch_h2c_wide_dbg(ctx->j->stream, d_m, d_out));
-  CK(d2h(ctx, out, d_out, 45 * sizeof(Fp)));
+  CK(d2h(ctx, out, d_out, 72 * sizeof(Fp) + 320 * 4));
   return 0;
 }
 

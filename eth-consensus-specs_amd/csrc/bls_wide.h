@@ -61,14 +61,21 @@ __device__ __forceinline__ int wpos() { return (int)(threadIdx.x & 31u); }  // l
 __device__ __forceinline__ int wdig() { return (int)(threadIdx.x & 15u); }  // digit index in D layout
 __device__ __forceinline__ int whalf() { return (int)((threadIdx.x >> 5) & 1u); }
 
-// DPP wave_shr:1 -- lane l gets lane l - 1, lane 0 gets 0 (lane 32 gets lane 31, which is always 0 here)
+// DPP wave_shr:1 -- lane l gets lane l - 1, lane 0 gets 0 (lane 32 gets lane 31, which is always 0 here).  The
+// move stays a separate v_mov_b32_dpp: folded by the compiler's DPP combine into the consuming VALU op
+// (v_add_u32_dpp ... wave_shr:1) it produced results shifted by one more lane in some contexts on gfx950
+// (found by tools/h2c_wide_debug.py: a carry-save normalisation came out as shr1(d & M + shr1(d >> 29))).
 __device__ __forceinline__ uint32_t shr1(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: invalid source -> 0
+  uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: invalid -> 0
+  asm volatile("" : "+v"(r));
+  return r;
 }
 // DPP row_newbcast:I -- every lane of a 16-lane row gets lane I of that row
 template <int I>
 __device__ __forceinline__ uint32_t rbc(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + I, 0xF, 0xF, true);
+  uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + I, 0xF, 0xF, true);
+  asm volatile("" : "+v"(r));  // no DPP combine (see shr1)
+  return r;
 }
 template <class F, int... I>
 __device__ __forceinline__ void for14_(F&& f, std::integer_sequence<int, I...>) {

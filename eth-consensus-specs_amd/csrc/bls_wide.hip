@@ -186,6 +186,39 @@ __global__ void __launch_bounds__(64) k_h2c_wide_dbg(const uint8_t* msg32, Fp* o
       chk(Y3, fp2_sub(f2mul(rr, fp2_sub(vv, x3)), fp2_dbl(f2mul(s1, jj))));
       const W2 ZZ = w2subk(K.k2, w2sqrk(K, w2add(wp.z, wq.z)), w2add(Z1, Z2));
       chk(ZZ, fp2_sub(fp2_sub(f2sqr(fp2_add(pl.z, ql.z)), z1), z2));
+      const W2 SZ = w2add(wp.z, wq.z);
+      chk(SZ, fp2_add(pl.z, ql.z));                                   // bit 16
+      const W2 SQ = w2sqrk(K, SZ);
+      chk(SQ, f2sqr(fp2_add(pl.z, ql.z)));                            // bit 17
+      chk(w2add(Z1, Z2), fp2_add(z1, z2));                            // bit 18
+      chk(w2subk(K.k2, SQ, w2add(Z1, Z2)), fp2_sub(f2sqr(fp2_add(pl.z, ql.z)), fp2_add(z1, z2)));  // bit 19
+      chk(w2subk(K.k1, SQ, w2add(Z1, Z2)), fp2_sub(f2sqr(fp2_add(pl.z, ql.z)), fp2_add(z1, z2)));  // bit 20
+      chk(W2{wsubk(K.k2, 0u, Z1.c0), 0u}, Fp2{fp_neg(z1.c0), fp_zero()});                          // bit 21
+      chk(W2{wnorm(K.k2), 0u}, fp2_zero());                                                       // bit 22
+      chk(Q.x, rl.x);                                                                             // bit 23
+      chk(Q.y, rl.y);                                                                             // bit 24
+      chk(Q.z, rl.z);                                                                             // bit 25
+      const G2A qw = j2w_to_aff(K, Q);
+      chk(w2_from_fp2(qw.x), ra.x);                                                               // bit 26
+      chk(w2_from_fp2(qw.y), ra.y);                                                               // bit 27
+      chk(w2mulk(K, ZZ, H), rl.z);                                                                // bit 28
+      {  // raw lanes of the c1 parts after slot 72: ZZ, SQ, Z1 + Z2, Z1, Z2
+        uint32_t* raw = reinterpret_cast<uint32_t*>(out + 72);
+        const W2 S12 = w2add(Z1, Z2);
+        raw[threadIdx.x] = ZZ.c1;
+        raw[64 + threadIdx.x] = SQ.c1;
+        raw[128 + threadIdx.x] = S12.c1;
+        raw[192 + threadIdx.x] = Z1.c1;
+        raw[256 + threadIdx.x] = Z2.c1;
+      }
+      {  // canonical raw values: P.z (own), Po.z, ZZ, H, Q.z, rl.z -- 12 Fp at slot 52
+        const Fp2 vals[9] = {w2_to_fp2(wp.z), w2_to_fp2(wq.z), w2_to_fp2(ZZ), w2_to_fp2(H), w2_to_fp2(Q.z), rl.z,
+                             w2_to_fp2(SQ), w2_to_fp2(Z1), w2_to_fp2(Z2)};
+        for (int q2 = 0; q2 < 9; q2++) {
+          dbg_put(out, 52 + 2 * q2, vals[q2].c0);
+          dbg_put(out, 53 + 2 * q2, vals[q2].c1);
+        }
+      }
       const int b0 = __builtin_amdgcn_readlane(bm, 0);
       if (threadIdx.x == 0) {
         Fp o = fp_zero();

@@ -18,7 +18,7 @@ def main():
     ctx = _native.context()
     for j in range(int(os.environ.get("N", "3"))):
         msg = hashlib.sha256(b"wide" + j.to_bytes(4, "little")).digest()
-        buf = ctypes.create_string_buffer(45 * 48)
+        buf = ctypes.create_string_buffer(72 * 48 + 320 * 4)
         ctx.check(ctx.lib.bls_test_h2c_wide_stages(ctx.h, msg, buf))
         v = [int.from_bytes(buf.raw[48 * k: 48 * k + 48], "little") for k in range(45)]
         u = O.hash_to_field_fp2(msg, 2, DST)
@@ -41,6 +41,18 @@ def main():
         res["z1z1"] = (v[37], v[38]) == (v[39], v[40])
         res["u1"] = (v[41], v[42]) == (v[43], v[44])
         print(j, res, flush=True)
+        w = [int.from_bytes(buf.raw[48 * k: 48 * k + 48], "little") for k in range(52, 70)]
+        f2 = [(w[2 * q], w[2 * q + 1]) for q in range(6)]
+        f2 = [(w[2 * q], w[2 * q + 1]) for q in range(9)]
+        pz, qz, zz, hh, qzz, rlz, sq, z1, z2 = f2
+        print("SQ ok", sq == O.f2_sqr(O.f2_add(pz, qz)), "Z1 ok", z1 == O.f2_sqr(pz), "Z2 ok", z2 == O.f2_sqr(qz), flush=True)
+        print("ZZ == 2 Pz Qz:", zz == O.f2_muls(O.f2_mul(pz, qz), 2), " Q.z == ZZ H:", qzz == O.f2_mul(zz, hh),
+              " rl.z == 2 Pz Qz H:", rlz == O.f2_mul(O.f2_muls(O.f2_mul(pz, qz), 2), hh), " Q.z == -rl.z:", qzz == O.f2_neg(rlz))
+        print("VALS", [hex(x) for x in w], flush=True)
+        import struct
+        raw = struct.unpack("<320I", buf.raw[72 * 48: 72 * 48 + 1280])
+        for name, b in (("ZZ1", 0), ("SQ1", 64), ("S121", 128), ("Z11", 192), ("Z21", 256)):
+            print(name, " ".join("%08x" % raw[b + l] for l in range(64)), flush=True)
         if not res["sswu0"]:
             print("  sswu0 got", hex(v[2])[:20], "want", hex(O.map_to_curve_sswu(u[0])[0][0])[:20])
 
