@@ -112,4 +112,4 @@ def test_wide_key_validate_edge_cases():
     for pk in keys:
         assert M.KeyValidate(pk) == OC.KeyValidate(pk), pk.hex()
     pks = [OC.SkToPk(k) for k in range(1, 516)]
-    assert M.AggregatePKs(pks) == OC.AggregatePKs(pks)
+    assert M._AggregatePKs(pks) == OC.AggregatePKs(pks)
