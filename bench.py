@@ -59,8 +59,8 @@ import time
 import numpy as np
 
 # before torch / HIP start (multi-GPU ranks initialise HIP through torch first): see _native.hw_queue_policy
-if not os.environ.get("BLSMI355X_KEEP_HW_QUEUES") and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 20:
-    os.environ["GPU_MAX_HW_QUEUES"] = "20"
+if not os.environ.get("BLSMI355X_KEEP_HW_QUEUES") and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "eth-consensus-specs_amd")):

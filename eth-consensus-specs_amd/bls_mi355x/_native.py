@@ -10,7 +10,7 @@ import ctypes
 import os
 import threading
 
-HW_QUEUES = 20  # 5 FAV jobs x 3 streams + the default/copy streams
+HW_QUEUES = 24  # 6 FAV jobs x 3 streams + the default/copy streams
 
 
 def hw_queue_policy() -> None:
@@ -110,6 +110,7 @@ _SIGS = {
     "bls_test_force_h2c_fallback": (_ip, [_vp, _u8p, _sz]),
     "bls_test_hash_to_g2_batch": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_test_wide_selftest": (_ip, [_vp, _u8p, _sz, _vp]),
+    "bls_test_final_check": (_ip, [_vp, _u8p, _sz, _ip, _vp]),
     "bls_test_hash_to_g2_wide": (_ip, [_vp, _u8p, _sz, _vp]),
     "bls_test_h2c_wide_stages": (_ip, [_vp, _u8p, _vp]),
 }

@@ -17,10 +17,10 @@ import numpy as np
 
 from . import _native
 
-# per-context job slots with streams: BLS_FAV_JOBS_INIT (default 5: 20 hardware queues cover its streams; 6 measured
-# 1.7 % faster at the end of round 2 but is not the default) of the
+# per-context job slots with streams: BLS_FAV_JOBS_INIT (default 6 with 24 hardware queues: the round-4 sweep,
+# profiles/r04e_jobs_sweep.txt -- 5:20 1.86-1.87 M/s, 6:24 1.91 M/s, 7:24 1.92-1.94 M/s, 8:32 collapses) of the
 # BLS_FAV_JOBS = 8 in include/blsmi355x.h, read by the library at bls_ctx_create
-FAV_JOBS = max(1, min(8, int(os.environ.get("BLS_FAV_JOBS_INIT", "5"))))
+FAV_JOBS = max(1, min(8, int(os.environ.get("BLS_FAV_JOBS_INIT", "6"))))
 # batches kept in flight by run_pipelined (<= FAV_JOBS)
 FAV_DEPTH = max(1, min(FAV_JOBS, int(os.environ.get("BLS_FAV_DEPTH", str(FAV_JOBS)))))
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # the BLS12-381 group order r

@@ -70,7 +70,8 @@ struct Job {
 
 struct bls_ctx {
   int device = 0;
-  int njobs = 5;  // job slots with streams: BLS_FAV_JOBS_INIT (default 5, at most BLS_FAV_JOBS)
+  bool fe_wide = true;  // final checks on the six-wave kernel (k_fe_wide); BLS_FE_WIDE=0: the one-wave k_fe_check
+  int njobs = 6;  // job slots with streams: BLS_FAV_JOBS_INIT (default 6, at most BLS_FAV_JOBS)
   Job jobs[BLS_FAV_JOBS];
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
@@ -255,7 +256,10 @@ int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
   Job& J = *ctx->j;
   HIPCK(hipEventRecord(J.ev_fe, J.stream));
   HIPCK(hipStreamWaitEvent(ctx->fe_stream, J.ev_fe, 0));
-  PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
+  if (ctx->fe_wide)
+    PROF2(7, ctx->fe_stream, launch_fe_wide(ctx->fe_stream, f, n, d_r));
+  else
+    PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
   int r = 0;
   HIPCK(hipMemcpyAsync(&r, d_r, sizeof r, hipMemcpyDeviceToHost, ctx->fe_stream));
   HIPCK(hipStreamSynchronize(ctx->fe_stream));
@@ -376,6 +380,7 @@ int bls_ctx_create(int device, bls_ctx** out) {
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   // All job streams are created here, before any kernel runs (streams created
   // later, between launches, were measured to hit HSA_STATUS_ERROR_OUT_OF_RESOURCES).
+  if (const char* v = getenv("BLS_FE_WIDE")) c->fe_wide = atoi(v) != 0;
   if (const char* v = getenv("BLS_FAV_JOBS_INIT")) c->njobs = atoi(v) < 1 ? 1 : atoi(v) > BLS_FAV_JOBS ? BLS_FAV_JOBS : atoi(v);
   for (int k = 0; k < c->njobs; ++k) {
     if (!job_init(c->jobs[k], prio_hi)) {
@@ -454,15 +459,13 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_OFFS, 2, d_offs);
   SCR(S_G1A, n, keys);
   SCR(S_OK, n + 2, ok);  // key verdicts | sig verdict | live
-  SCR(S_PC_P, 3, P);  // P[0] apk, P[1] -G1 (k_percall_pairs); P[2] -G1 for stream3's Miller loop
+  SCR(S_PC_P, 2, P);  // P[0] apk, P[1] -G1 (k_percall_pairs)
   SCR(S_G2A, 2, Q);
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
   SCR(S_AV_HCF, h2c_scratch_fd(1), hf);
   SCR(S_AV_FLAG, 1, flag);
   SCR(S_F, 3, f);  // f(apk, H) | f(-G1, sigma) | their product
-  uint32_t* L;
-  SCR(S_PC_L, lines_wide_u32(2), L);  // line records of the two pairs (F2 layout)
   SCR(S_INT, 4, d_r);
   uint8_t* d_pk = d_in;
   uint8_t* d_sig = d_in + 48 * n;
@@ -484,19 +487,14 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate_wide(st3, d_sig, 1, Q + 1, ok + n));
   HIPCK(hipEventRecord(J.ev_sig, st3));
-  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, P + 2);
-  LK(hipGetLastError());
-  // the G2 side of the Miller loop of (-G1, sigma) while hash_to_G2 runs (a rejected signature: constant lines)
-  LK(launch_lines_wide(st3, P + 2, Q + 1, ok + n, 1, L + lines_wide_u32(1)));
-  HIPCK(hipEventRecord(J.ev_msm, st3));
   LK(launch_keys(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
-  LK(launch_lines_wide(st, P, Q, nullptr, 1, L));  // rejected inputs are identities here; `live` decides
-  HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
-  LK(launch_facc_wide(st, L, 2, f + 2));  // f(apk, H) f(-G1, sigma), one shared squaring per step
+  // both pairs' Miller loop on one workgroup: (apk, H) -- rejected inputs are identities there, `live` decides --
+  // and (-G1, sigma), constant lines for a rejected signature
+  LK(launch_miller_wide(st, P, Q, nullptr, ok + n, 2, f + 2));
   int live = 0;
   HIPCK(hipMemcpyAsync(&live, ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
   const int fe = run_final_check(ctx, f + 2);  // orders after st
@@ -771,6 +769,28 @@ int bls_test_hash_to_g2_wide(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint
   hipLaunchKernelGGL(k_g2_compress_many, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, n, H, d_out);
   LK(hipGetLastError());
   CK(d2h(ctx, out96, d_out, 96 * n));
+  return 0;
+}
+
+// final-exponentiation check of the product of n raw Fp12 values (576 bytes each: 12 little-endian Montgomery Fp,
+// tower order) with the six-wave kernel (wide != 0) or the one-wave lane kernel: *out = 1 / 0
+int bls_test_final_check(bls_ctx* ctx, const uint8_t* f576, size_t n, int wide, int32_t* out) {
+  API_ENTER(ctx);
+  if (!f576 || !out || !n || n > 64) return BLS_E_ARG;
+  Fp12* d_f;
+  int* d_r;
+  SCR(S_F, n, d_f);
+  SCR(S_INT, 4, d_r);
+  hipStream_t st = ctx->j->stream;
+  CK(h2d(ctx, d_f, f576, 576 * n));
+  uint64_t* d_ts = nullptr;
+  if (wide == 2) SCR(S_OFFS, 16, d_ts);
+  if (wide)
+    LK(launch_fe_wide(st, d_f, (int)n, d_r, d_ts));
+  else
+    LK(launch_final_check_wave(st, d_f, (int)n, d_r));
+  CK(d2h(ctx, out, d_r, sizeof(int32_t)));
+  if (d_ts) CK(d2h(ctx, out + 2, d_ts, 8 * 8));
   return 0;
 }
 

@@ -1,0 +1,217 @@
+// k_fe_wide: the final-exponentiation check with the hard part in wavefront-cooperative arithmetic (bls_wide.h,
+// F2 layout) on six waves -- the per-call path's check.  Same schedule, same answer as k_fe_check
+// (bls_fe.hip), which stays the batch / bisection check.
+#include "bls_kernels.h"
+#include "bls_lane.h"
+#include "bls_wide.h"
+#include "bls_wide_g2.h"
+#include "bls_fe.h"
+
+namespace bls {
+
+using namespace wide;
+
+// ---- final-exponentiation check: easy part lane-parallel, hard part in F2 layout on six waves ----------
+// Wave 0 runs the product of the partials and the easy part with the lane-parallel phase executor of bls_fe.h
+// (the other waves only keep the barriers); the result t = f^((p^6 - 1)(p^2 + 1)) then moves into six LDS rows
+// of F2-layout values (wave k owns the w^k coefficient), and the hard part -- four x-power chains of cyclotomic
+// squarings (Granger-Scott: per w^k one or two Fp2 products), Fp12 products (six per wave), Frobenius maps and
+// conjugations, in fe_schedule's order -- runs with every wave forming its coefficient of each result.  Every
+// bank value is brought below 2.0001p after each operation (a product by R mod p), so the cyclotomic
+// formula's 3 t - 2 a and the products' xi terms subtract small values against 64p.
+// gamma1_k = xi^(k (p - 1) / 6) (A^p: w^k coefficient -> conj(c_k) gamma1_k) and gamma2_k = gamma1_k conj(gamma1_k)
+// (real), per w-basis index k
+__device__ static const Fp2 FE_W_G1[6] = {FROB1_0, FROB1_1, FROB1_2, FROB1_3, FROB1_4, FROB1_5};
+__device__ static const Fp2 FE_W_G2[6] = {FROB2_0, FROB2_1, FROB2_2, FROB2_3, FROB2_4, FROB2_5};
+
+struct FeWide {
+  uint32_t* B;  // banks: B[(bank * 6 + k) * 64 + lane]
+  int k, lane;
+  WKG K;
+  uint32_t two, mtwo;  // 2 and -2 (Montgomery form, both halves)
+  __device__ uint32_t ld(int bank, int j) const { return B[(bank * 6 + j) * 64 + lane]; }
+  // publish this wave's coefficient of bank d; an operation whose destination is also a source waits for every
+  // wave's reads first, otherwise the barrier after the previous write already ordered them
+  __device__ void put(int d, uint32_t v, bool inplace) {
+    if (inplace) __syncthreads();
+    B[(d * 6 + k) * 64 + lane] = v;
+    __syncthreads();
+  }
+  __device__ uint32_t xi(uint32_t v) const { return wf_xi(K.k256, v); }
+  __device__ uint32_t real(uint32_t v) const { return whalf() ? 0u : v; }  // v in half 0 only (a real Fp2)
+  // D = A B: coefficient k = sum_{i <= k} a_i b_{k-i} + sum_{i > k} a_i (xi b_{k-i+6}), twelve wmac terms per
+  // half into one reduction
+  __device__ void mul(int a, int b, int d) {
+    uint64_t acc = 0;
+#pragma unroll 1
+    for (int i = 0; i < 6; i++) {
+      const int j = k - i < 0 ? k - i + 6 : k - i;
+      const uint32_t bj = ld(b, j);
+      wf_mac(acc, K.kneg, ld(a, i), i > k ? xi(bj) : bj);
+    }
+    put(d, wredc(acc), d == a || d == b);
+  }
+  // D = A^2, A cyclotomic (Granger-Scott on the Fp4 pairs (a_k, a_k+3), bls_fe.h / tools/gen_fe.py op_cyc):
+  //   a0' = 3 (a0^2 + xi a3^2) - 2 a0,  a3' = 6 a0 a3 + 2 a3,  a2' = 3 (a1^2 + xi a4^2) - 2 a2,  a5' = 6 a1 a4 + 2 a5,
+  //   a4' = 3 (a2^2 + xi a5^2) - 2 a4,  a1' = 6 xi a2 a5 + 2 a1
+  // each as ONE reduction of a few products, the linear terms folded in as products by the constants +-2:
+  //   a0' = a0 (3 a0 - 2) + (3 xi a3) a3,  a3' = a3 (6 a0 + 2),  a2' = a1 (3 a1) + (3 xi a4) a4 + a2 (-2),
+  //   a5' = a1 (6 a4) + a5 2,  a4' = a2 (3 a2) + (3 xi a5) a5 + a4 (-2),  a1' = (6 xi a2) a5 + a1 2
+  __device__ void cyc(int a, int d) {
+    const int m = k == 0 || k == 3 ? 0 : (k == 2 || k == 5 ? 1 : 2);  // the pair (m, m + 3) this output needs
+    const uint32_t x = ld(a, m), y = ld(a, m + 3);
+    uint64_t acc = 0;
+    if (k == 0) {
+      wf_mac(acc, K.kneg, x, wnorm(wmuls<3>(x) + real(wnorm(K.k1 - two))));
+      wf_mac(acc, K.kneg, wmuls<3>(xi(y)), y);
+    } else if (k == 3) {
+      wf_mac(acc, K.kneg, y, wnorm(wmuls<6>(x) + real(two)));
+    } else if (k == 2 || k == 4) {
+      wf_mac(acc, K.kneg, x, wmuls<3>(x));
+      wf_mac(acc, K.kneg, wmuls<3>(xi(y)), y);
+      wf_mac_fp(acc, ld(a, k), mtwo);
+    } else if (k == 5) {
+      wf_mac(acc, K.kneg, x, wmuls<6>(y));
+      wf_mac_fp(acc, ld(a, 5), two);
+    } else {  // k == 1
+      wf_mac(acc, K.kneg, wmuls<6>(xi(x)), y);
+      wf_mac_fp(acc, ld(a, 1), two);
+    }
+    put(d, wredc(acc), d == a);
+  }
+  // conjugation: the odd coefficients negated (64 p - v: sources are product outputs, below 1.1 p)
+  __device__ void conj(int a, int d) {
+    const uint32_t v = ld(a, k);
+    put(d, (k & 1) ? wnorm(K.k1 - v) : v, d == a);
+  }
+  __device__ void frob1(int a, int d, uint32_t g) {  // conj(a_k) gamma1_k
+    uint64_t acc = 0;
+    wf_mac(acc, K.kneg, wf_conj(K.k256, ld(a, k)), g);
+    put(d, wredc(acc), d == a);
+  }
+  __device__ void frob2(int a, int d, uint32_t g2) {  // a_k gamma2_k (gamma2_k in Fp: both halves)
+    uint64_t acc = 0;
+    wf_mac_fp(acc, ld(a, k), g2);
+    put(d, wredc(acc), d == a);
+  }
+  // dst = src^x = conj(src^|x|): the chain ping-pongs between dst and tmp so each step has one barrier
+  __device__ void powx(int src, int dst, int tmp) {
+    int acc = src, o = dst;
+#pragma unroll 1
+    for (int i = 62; i >= 0; --i) {
+      cyc(acc, o);
+      acc = o;
+      o = o == dst ? tmp : dst;
+      if ((X_ABS >> i) & 1ull) {
+        mul(acc, src, o);
+        acc = o;
+        o = o == dst ? tmp : dst;
+      }
+    }
+    conj(acc, dst);
+  }
+};
+
+// the easy part on wave 0 (bls_fe.h executor), barriers kept by all six waves
+struct FeEasy : FeOps<FeEasy> {
+  FeSlot* s;
+  int lane;
+  bool active;
+  template <int KIND, int NX, int NY>
+  __device__ void ph(int phase, int a, int b, int d) {
+    if (active) {
+      const FeDesc<NX, NY> w = fe_desc<NX, NY>(phase, lane);
+      fe_lane<KIND, NX, NY>(s, w.w, a, b, d);
+    }
+    __syncthreads();
+  }
+};
+
+__global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const uint32_t* sel, int* out, uint64_t* ts) {
+  int nts = 0;
+  auto stamp = [&]() {
+    if (ts && threadIdx.x == 0) ts[nts] = wall_clock64();
+    nts++;
+  };
+  stamp();
+  __shared__ FeSlot s[FE_NSLOT];
+  __shared__ uint32_t B[7 * 6 * 64];
+  __shared__ int bad;
+  const int lane = wlane(), k = (int)(threadIdx.x >> 6);
+  if (sel) {
+    fin += sel[blockIdx.x];
+    out += blockIdx.x;
+  }
+  if (k == 0) {
+    fe_load_consts(s, lane, 64);
+    if (lane == 0) {
+      bad = 0;
+      fe_st(s, FE_ABS_BASE + FE_CS, fq_zero());
+    }
+  }
+  FeEasy ex;
+  ex.s = s;
+  ex.lane = lane;
+  ex.active = k == 0;
+  __syncthreads();
+  for (int i = 0; i < n; i++) {
+    if (k == 0 && lane < 12) fe_st(s, 12 * (i ? 1 : 0) + lane, fq_unpack(reinterpret_cast<const Fp*>(fin + i)[lane]));
+    __syncthreads();
+    if (i) ex.mul(0, 1, 0);
+  }
+  stamp();
+  ex.easy(0, 2);
+  ex.easy_back(2, 0);
+  ex.frob2(0, 1);
+  ex.mul(1, 0, 0);  // bank 0 = t
+  stamp();
+  // t -> F2 layout: w^k is the tower Fp2 (k & 1) * 3 + (k >> 1), Fp slots 2 t, 2 t + 1
+  FeWide W;
+  W.B = B;
+  W.k = k;
+  W.lane = lane;
+  W.K = wkg_init();
+  W.two = wmuls<2>(W.K.one);
+  W.mtwo = wnorm(W.K.k1 - W.two);
+  {
+    const int tp = (k & 1) * 3 + (k >> 1);
+    const int j = lane & 15;
+    const uint32_t dgt = j < 14 ? s[2 * tp + (lane >> 5)].d[j] : 0u;
+    B[(0 * 6 + k) * 64 + lane] = wmul(dgt, W.K.one);  // N-form digits -> W form, below 1.1 p
+  }
+  __syncthreads();
+  const uint32_t wg1 = wf_from_fp2(FE_W_G1[k]), wg2 = w_from_fp(FE_W_G2[k].c0);
+  // hard part, bls_fe.h fe_schedule's order (banks 0..5)
+  W.powx(0, 1, 6);      // 1 = t^x
+  stamp();
+  W.conj(0, 3);
+  W.mul(3, 1, 2);    // 2 = a = t^(x-1)
+  W.powx(2, 1, 6);      // 1 = a^x
+  W.conj(2, 3);
+  W.mul(1, 3, 2);    // 2 = a = t^((x-1)^2)
+  W.powx(2, 1, 6);      // 1 = a^x
+  W.frob1(2, 3, wg1);  // 3 = a^p
+  W.mul(3, 1, 3);    // 3 = b = a^(x+p)
+  W.powx(3, 1, 6);      // 1 = b^x
+  W.powx(1, 4, 6);      // 4 = b^(x^2)
+  W.frob2(3, 5, wg2);  // 5 = b^(p^2)
+  W.mul(4, 5, 1);
+  W.conj(3, 4);      // 4 = b^-1
+  W.mul(1, 4, 1);    // 1 = c = b^(x^2+p^2-1)
+  W.cyc(0, 5);
+  W.mul(5, 0, 5);    // 5 = t^3
+  W.mul(1, 5, 1);    // 1 = c t^3
+  stamp();
+  const Fp2 v = wf_to_fp2(W.ld(1, k));
+  const bool ok = k == 0 ? (fp_is_one(v.c0) && fp_is_zero(v.c1)) : (fp_is_zero(v.c0) && fp_is_zero(v.c1));
+  if (lane == 0 && !ok) atomicOr(&bad, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = bad ? 0 : 1;
+}
+
+hipError_t launch_fe_wide(hipStream_t st, const Fp12* f, int n, int* out, uint64_t* ts) {
+  hipLaunchKernelGGL(k_fe_wide, dim3(1), dim3(384), 0, st, f, n, (const uint32_t*)nullptr, out, ts);
+  return hipGetLastError();
+}
+
+}  // namespace bls

@@ -101,6 +101,12 @@ hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t 
 hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L);
 hipError_t launch_facc_wide(hipStream_t st, const uint32_t* L, int npairs, Fp12* out);
 size_t lines_wide_u32(size_t n);
+// the whole Miller loop of npairs <= 2 pairs on one workgroup (line waves + six f waves): out = f (tower Fp12);
+// ok0 / ok1 (nullable): pair 0 / 1 runs with constant lines unless *okp
+hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
+                              Fp12* out);
+// final-exponentiation check of the product of f[0 .. n): easy part lane-parallel, hard part on six waves (F2)
+hipError_t launch_fe_wide(hipStream_t st, const Fp12* f, int n, int* out, uint64_t* ts = nullptr);  // ts: stage clocks (tests)
 // KeyValidate with two keys per wave (k_key_validate semantics)
 hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok);
 

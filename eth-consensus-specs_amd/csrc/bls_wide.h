@@ -65,16 +65,20 @@ __device__ __forceinline__ int whalf() { return (int)((threadIdx.x >> 5) & 1u); 
 // move stays a separate v_mov_b32_dpp: folded by the compiler's DPP combine into the consuming VALU op
 // (v_add_u32_dpp ... wave_shr:1) it produced results shifted by one more lane in some contexts on gfx950
 // (found by tools/h2c_wide_debug.py: a carry-save normalisation came out as shr1(d & M + shr1(d >> 29))).
+// an opaque copy: keeps each DPP move a separate instruction (the compiler's DPP combine folded wave_shr moves
+// into their VALU consumers and shifted a normalisation by one more lane on gfx950)
+// (a plain asm measured the same as the volatile one: tools/fe_stages.py, round 4)
+#define BLS_WIDE_FENCE(r) asm volatile("" : "+v"(r))
 __device__ __forceinline__ uint32_t shr1(uint32_t v) {
   uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);  // bound_ctrl: invalid -> 0
-  asm volatile("" : "+v"(r));
+  BLS_WIDE_FENCE(r);
   return r;
 }
 // DPP row_newbcast:I -- every lane of a 16-lane row gets lane I of that row
 template <int I>
 __device__ __forceinline__ uint32_t rbc(uint32_t v) {
   uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + I, 0xF, 0xF, true);
-  asm volatile("" : "+v"(r));  // no DPP combine (see shr1)
+  BLS_WIDE_FENCE(r);  // no DPP combine (see shr1)
   return r;
 }
 template <class F, int... I>
@@ -149,6 +153,13 @@ __device__ __forceinline__ uint32_t wdot2(uint32_t x, uint32_t y, uint32_t u, ui
   wmac(a, x, y);
   wmac(a, u, v);
   return wredc(a);
+}
+
+// carry-save round on column sums (same value, columns < 2^29 + 2^35): lets a dot product take two more wmac
+// terms (the column bound 2^63 of wredc holds for at most two wmac between rounds)
+__device__ __forceinline__ void wacc_norm(uint64_t& acc) {
+  const uint64_t h = acc >> 29;  // < 2^34
+  acc = (acc & WM) + (((uint64_t)shr1((uint32_t)(h >> 32)) << 32) | shr1((uint32_t)h));
 }
 
 // per-lane constants of a kernel: the subtraction constant 64 p (Q29_K1) and R mod p (one) in D layout
@@ -279,6 +290,21 @@ __device__ __forceinline__ uint32_t wf_mul(uint32_t kn, uint32_t a, uint32_t b) 
   const uint32_t sa = wswap(a), sb = wswap(b);
   const uint32_t nb1 = wnorm(kn - sb);
   return wdot2(h ? sa : a, b, h ? a : sa, h ? sb : nb1);
+}
+// acc += a b (F2 layout, unreduced column sums; kn covering b1), then a carry-save round: any number of these
+// terms can share one wredc while their values sum below p R
+__device__ __forceinline__ void wf_mac(uint64_t& acc, uint32_t kn, uint32_t a, uint32_t b) {
+  const bool h = whalf() != 0;
+  const uint32_t sa = wswap(a), sb = wswap(b);
+  const uint32_t nb1 = wnorm(kn - sb);
+  wmac(acc, h ? sa : a, b);
+  wmac(acc, h ? a : sa, h ? sb : nb1);
+  wacc_norm(acc);
+}
+// acc += a c for an Fp constant c held in both halves (the Fp2 a times a real scalar: one wmac)
+__device__ __forceinline__ void wf_mac_fp(uint64_t& acc, uint32_t a, uint32_t c) {
+  wmac(acc, a, c);
+  wacc_norm(acc);
 }
 // (a0 + a1)(a0 - a1 + ks) in half 0, a0 (2 a1) in half 1 (ks covering a1)
 __device__ __forceinline__ uint32_t wf_sqr(uint32_t ks, uint32_t a) {

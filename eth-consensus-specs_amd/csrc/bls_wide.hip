@@ -481,62 +481,80 @@ constexpr int MLW_STEPS = 68;  // 63 doublings + 5 additions
 // < 2.0001): doubling in X < 516, Y, Z < 66 -> X3 < 516, Y3, Z3 < 66; addition -> all < 66; lines l0 < 66,
 // l2 and l3 products.  Subtraction constants: 64p for products and small sums, 256p / 512p / 1024p where the
 // subtrahend is a coordinate; the Fp2 products negate with 4096p (kneg), squarings with 2048p.
+struct LineW {
+  uint32_t X, Y, Z, xQ, yQ, nxP, yP;
+  __device__ void init(const G1A& P, const G2A& Q, bool live) {
+    const G2A q = live ? Q : g2_generator();
+    nxP = live ? w_from_fp(fp_neg(P.x)) : 0u;
+    yP = live ? w_from_fp(P.y) : 0u;
+    xQ = wf_from_fp2(q.x);
+    yQ = wf_from_fp2(q.y);
+    X = xQ;
+    Y = yQ;
+    Z = wf_from_fp2(fp2_one());
+  }
+  // doubling step: T = 2T, the record (l0, l2, l3) into o[0], o[64], o[128]
+  __device__ void dbl(const WKG& K, uint32_t* o) {
+    const uint32_t kn = K.kneg, ks = K.k2048_2;
+    const uint32_t A = wf_sqr(ks, X), B = wf_sqr(ks, Y), C = wf_sqr(ks, B);
+    const uint32_t XB = wf_sqr(ks, wadd(X, B));
+    const uint32_t D = wmuls<2>(wsubk(K.k1, XB, wadd(A, C)));
+    const uint32_t E = wmuls<3>(A);
+    const uint32_t F = wf_sqr(ks, E), ZZ = wf_sqr(ks, Z);
+    const uint32_t l0 = wsubk(K.k1, wf_mul(kn, E, X), wmuls<2>(B));
+    const uint32_t l2 = wmul(wf_mul(kn, E, ZZ), nxP);
+    const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Y, Z)), wadd(B, ZZ));
+    const uint32_t l3 = wmul(wf_mul(kn, z3, ZZ), yP);
+    const uint32_t x3 = wsubk(K.k512_2, F, wmuls<2>(D));
+    const uint32_t y3 = wsubk(K.k1, wf_mul(kn, E, wsubk(K.k1024, D, x3)), wmuls<8>(C));
+    X = x3;
+    Y = y3;
+    Z = z3;
+    o[0] = l0;
+    o[64] = l2;
+    o[128] = l3;
+  }
+  // addition of Q (affine): T = T + Q, the record into o
+  __device__ void add(const WKG& K, uint32_t* o) {
+    const uint32_t kn = K.kneg, ks = K.k2048_2;
+    const uint32_t z1z1 = wf_sqr(ks, Z);
+    const uint32_t u2 = wf_mul(kn, xQ, z1z1);
+    const uint32_t s2 = wf_mul(kn, wf_mul(kn, yQ, Z), z1z1);
+    const uint32_t h = wsubk(K.k1024, u2, X);
+    const uint32_t hh = wf_sqr(ks, h);
+    const uint32_t i4 = wmuls<4>(hh);
+    const uint32_t j = wf_mul(kn, h, i4);
+    const uint32_t r = wmuls<2>(wsubk(K.k256, s2, Y));
+    const uint32_t v = wf_mul(kn, X, i4);
+    const uint32_t x3 = wsubk(K.k1, wf_sqr(ks, r), wadd(j, wmuls<2>(v)));
+    const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, Y, j)));
+    const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Z, h)), wadd(z1z1, hh));
+    const uint32_t l0 = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
+    o[0] = l0;
+    o[64] = wmul(r, nxP);
+    o[128] = wmul(z3, yP);
+    X = x3;
+    Y = y3;
+    Z = z3;
+  }
+};
+
 __global__ void __launch_bounds__(64) k_lines_wide(const G1A* P, const G2A* Q, const int* ok, size_t n,
                                                    uint32_t* L) {
   const size_t i = blockIdx.x;
   if (i >= n) return;
   const WKG K = wkg_init();
   const int lane = wlane();
-  const bool live = (!ok || ok[i]) && !P[i].inf && !Q[i].inf;
-  const G2A q = live ? Q[i] : g2_generator();
-  const uint32_t nxP = live ? w_from_fp(fp_neg(P[i].x)) : 0u, yP = live ? w_from_fp(P[i].y) : 0u;
-  const uint32_t xQ = wf_from_fp2(q.x), yQ = wf_from_fp2(q.y);
-  uint32_t X = xQ, Y = yQ, Z = wf_from_fp2(fp2_one());
+  LineW T;
+  T.init(P[i], Q[i], (!ok || ok[i]) && !P[i].inf && !Q[i].inf);
   uint32_t* o = L + (size_t)i * MLW_STEPS * 3 * 64 + lane;
-  const uint32_t kn = K.kneg, ks = K.k2048_2;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
-    {  // doubling
-      const uint32_t A = wf_sqr(ks, X), B = wf_sqr(ks, Y), C = wf_sqr(ks, B);
-      const uint32_t XB = wf_sqr(ks, wadd(X, B));
-      const uint32_t D = wmuls<2>(wsubk(K.k1, XB, wadd(A, C)));
-      const uint32_t E = wmuls<3>(A);
-      const uint32_t F = wf_sqr(ks, E), ZZ = wf_sqr(ks, Z);
-      const uint32_t l0 = wsubk(K.k1, wf_mul(kn, E, X), wmuls<2>(B));
-      const uint32_t l2 = wmul(wf_mul(kn, E, ZZ), nxP);
-      const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Y, Z)), wadd(B, ZZ));
-      const uint32_t l3 = wmul(wf_mul(kn, z3, ZZ), yP);
-      const uint32_t x3 = wsubk(K.k512_2, F, wmuls<2>(D));
-      const uint32_t y3 = wsubk(K.k1, wf_mul(kn, E, wsubk(K.k1024, D, x3)), wmuls<8>(C));
-      X = x3;
-      Y = y3;
-      Z = z3;
-      o[0] = l0;
-      o[64] = l2;
-      o[128] = l3;
+    T.dbl(K, o);
+    o += 3 * 64;
+    if ((X_ABS >> b) & 1ull) {
+      T.add(K, o);
       o += 3 * 64;
-    }
-    if ((X_ABS >> b) & 1ull) {  // addition of Q (affine)
-      const uint32_t z1z1 = wf_sqr(ks, Z);
-      const uint32_t u2 = wf_mul(kn, xQ, z1z1);
-      const uint32_t s2 = wf_mul(kn, wf_mul(kn, yQ, Z), z1z1);
-      const uint32_t h = wsubk(K.k1024, u2, X);
-      const uint32_t hh = wf_sqr(ks, h);
-      const uint32_t i4 = wmuls<4>(hh);
-      const uint32_t j = wf_mul(kn, h, i4);
-      const uint32_t r = wmuls<2>(wsubk(K.k256, s2, Y));
-      const uint32_t v = wf_mul(kn, X, i4);
-      const uint32_t x3 = wsubk(K.k1, wf_sqr(ks, r), wadd(j, wmuls<2>(v)));
-      const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, Y, j)));
-      const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Z, h)), wadd(z1z1, hh));
-      const uint32_t l0 = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
-      o[0] = l0;
-      o[64] = wmul(r, nxP);
-      o[128] = wmul(z3, yP);
-      o += 3 * 64;
-      X = x3;
-      Y = y3;
-      Z = z3;
     }
   }
 }
@@ -609,6 +627,113 @@ __global__ void __launch_bounds__(384) k_facc_wide(const uint32_t* L, int npairs
     Fp2& dst = (k >> 1) == 0 ? h6.c0 : ((k >> 1) == 1 ? h6.c1 : h6.c2);
     dst = v;
   }
+}
+
+// Fused per-call Miller loop: waves 0..5 accumulate f (as k_facc_wide, each f^2 and f l as ONE reduction of
+// lazily summed products, f ping-ponging between two LDS banks), wave 6 + p runs pair p's G2 side (LineW) and
+// writes its line records into LDS.  The two sides meet through per-pair progress counters (release / acquire at
+// workgroup scope); the six f waves synchronise among themselves through a counter barrier, since the line waves
+// never join an s_barrier after the start.  The line records of all steps fit in LDS (2 x 68 x 768 B).
+constexpr int MLF_PAIRS = 2;
+struct WaveBar {  // barrier of the first nw waves of the workgroup: cnt counts arrivals, gen is this wave's target
+  int* cnt;
+  int gen, nw;
+  __device__ void sync() {
+    gen += nw;
+    if (wlane() == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+  }
+};
+
+__global__ void __launch_bounds__(64 * (6 + MLF_PAIRS)) k_miller_wide(const G1A* P, const G2A* Q, const int* ok0,
+                                                                      const int* ok1, int npairs, Fp12* out) {
+  __shared__ uint32_t lr[MLF_PAIRS][MLW_STEPS][3 * 64];
+  __shared__ uint32_t fs[2][6 * 64];
+  __shared__ int prog[MLF_PAIRS];
+  __shared__ int barc;
+  const WKG K = wkg_init();
+  const int lane = wlane(), k = (int)(threadIdx.x >> 6);
+  if (threadIdx.x < MLF_PAIRS) prog[threadIdx.x] = 0;
+  if (threadIdx.x == 0) barc = 0;
+  if (k < 6) fs[0][k * 64 + lane] = k == 0 ? wf_from_fp2(fp2_one()) : 0u;
+  __syncthreads();
+  if (k >= 6) {  // G2 side of pair k - 6
+    const int pi = k - 6;
+    if (pi >= npairs) return;
+    LineW T;
+    const int* okp = pi ? ok1 : ok0;
+    T.init(P[pi], Q[pi], (!okp || *okp) && !P[pi].inf && !Q[pi].inf);
+    int step = 0;
+#pragma unroll 1
+    for (int b = 62; b >= 0; --b) {
+      T.dbl(K, &lr[pi][step][lane]);
+      ++step;
+      if (lane == 0) __hip_atomic_store(&prog[pi], step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((X_ABS >> b) & 1ull) {
+        T.add(K, &lr[pi][step][lane]);
+        ++step;
+        if (lane == 0) __hip_atomic_store(&prog[pi], step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    return;
+  }
+  WaveBar bar{&barc, 0, 6};
+  const uint32_t kn = K.kneg;
+  int c = 0, step = 0;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) {  // f = f^2: sum over FSQ_TERMS of (m a_i, xi on wrap) a_j
+      const uint32_t* f = fs[c];
+      uint64_t acc = 0;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const uint32_t ii = FSQ_TERMS[k][t][0], jj = FSQ_TERMS[k][t][1], m = FSQ_TERMS[k][t][2];
+        if (!m) continue;
+        uint32_t x = f[ii * 64 + lane];
+        x = m == 2 ? wmuls<2>(x) : x;
+        x = FSQ_TERMS[k][t][3] ? wf_xi(K.k256, x) : x;
+        wf_mac(acc, kn, x, f[jj * 64 + lane]);
+      }
+      fs[c ^ 1][k * 64 + lane] = wredc(acc);
+      c ^= 1;
+      bar.sync();
+    }
+    const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
+#pragma unroll 1
+    for (int sl = 0; sl < nl; ++sl, ++step) {
+#pragma unroll 1
+      for (int pi = 0; pi < npairs; ++pi) {
+        while (__hip_atomic_load(&prog[pi], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= step)
+          __builtin_amdgcn_s_sleep(1);
+        const uint32_t* l = &lr[pi][step][lane];
+        const uint32_t* f = fs[c];
+        const int i2 = k < 2 ? k + 4 : k - 2, i3 = k < 3 ? k + 3 : k - 3;
+        uint64_t acc = 0;
+        wf_mac(acc, kn, f[k * 64 + lane], l[0]);
+        const uint32_t f2 = f[i2 * 64 + lane], f3 = f[i3 * 64 + lane];
+        wf_mac(acc, kn, k < 2 ? wf_xi(K.k256, f2) : f2, l[64]);
+        wf_mac(acc, kn, k < 3 ? wf_xi(K.k256, f3) : f3, l[128]);
+        fs[c ^ 1][k * 64 + lane] = wredc(acc);
+        c ^= 1;
+        bar.sync();
+      }
+    }
+  }
+  // x < 0: conjugate (negate the odd w-coefficients); canonical Fp2 into the tower slot of w^k
+  const uint32_t v0 = fs[c][k * 64 + lane];
+  const Fp2 v = wf_to_fp2((k & 1) ? wnorm(K.k1 - v0) : v0);  // f values below 1.1 p
+  if (lane == 0) {
+    Fp6& h6 = (k & 1) ? out->c1 : out->c0;
+    Fp2& dst = (k >> 1) == 0 ? h6.c0 : ((k >> 1) == 1 ? h6.c1 : h6.c2);
+    dst = v;
+  }
+}
+
+hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
+                              Fp12* out) {
+  if (npairs < 1 || npairs > MLF_PAIRS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L) {

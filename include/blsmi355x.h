@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct bls_ctx bls_ctx;
 
-/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 5) get streams. */
+/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 6) get streams. */
 #define BLS_FAV_JOBS 8
 
 /* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
@@ -287,6 +287,12 @@ int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uin
 int bls_test_hash_to_g2_wide(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96);
 /* intermediate stages of the one-wave hash of one 32-byte message (debugging) */
 int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out);
+/* bls_test_final_check: the final-exponentiation check (FE(f_0 .. f_{n-1}) == 1) of n <= 64 raw Fp12 values
+ * (576 bytes each: 12 little-endian Montgomery Fp in tower order) on the six-wave kernel (wide != 0) or the
+ * one-wave lane kernel; *out = 1 / 0.  wide == 2: also the six-wave kernel's stage clocks (wall_clock64, 100 MHz)
+ * as 8 uint64 at out + 2 (out then needs room for 18 int32). */
+int bls_test_final_check(bls_ctx* ctx, const uint8_t* f576, size_t n, int wide, int32_t* out);
+
 /* bls_test_wide_selftest: nw waves compare the wavefront-cooperative products
  * (bls_wide.h) with the lane form on four inputs each (48-byte big-endian
  * integers < p); bad[w] = bitmask of differing forms, 0 when all agree. */

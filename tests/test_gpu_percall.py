@@ -113,3 +113,42 @@ def test_wide_key_validate_edge_cases():
         assert M.KeyValidate(pk) == OC.KeyValidate(pk), pk.hex()
     pks = [OC.SkToPk(k) for k in range(1, 516)]
     assert M._AggregatePKs(pks) == OC.AggregatePKs(pks)
+
+
+def test_fe_wide_matches_lane_kernel():
+    """The six-wave final-exponentiation check (k_fe_wide, hard part in F2 layout) against the one-wave lane kernel
+    and known answers without a pairing: FE(f) = 1 for every f in Fp6 (p^6 - 1 divides (p^12 - 1) / r), so
+    f conj(f) (in Fp6) and Fp6 elements pass, while a random Fp12 value, f f, and f times a perturbed conjugate
+    fail.  Partial counts 1, 2 and 5 (the product inside the kernel)."""
+    import ctypes
+
+    from bls_mi355x import _native
+
+    ctx = _native.context()
+    rnd = random.Random(0xFE12)
+
+    def raw(c):  # 12 Montgomery-form residues (any residue is some element's Montgomery form)
+        return b"".join(v.to_bytes(48, "little") for v in c)
+
+    def conj(c):
+        return c[:6] + [(O.P - v) % O.P for v in c[6:]]
+
+    def check(fs, wide):
+        out = ctypes.c_int32(-1)
+        ctx.check(ctx.lib.bls_test_final_check(ctx.h, b"".join(raw(f) for f in fs), len(fs), wide, ctypes.byref(out)))
+        return out.value
+
+    cases = []
+    for _ in range(3):
+        f = [rnd.randrange(O.P) for _ in range(12)]
+        g = [rnd.randrange(O.P) for _ in range(6)] + [0] * 6
+        h = [rnd.randrange(O.P) for _ in range(12)]
+        cases += [([f], 0), ([g], 1), ([f, conj(f)], 1), ([f, f], 0), ([f, g, conj(f)], 1),
+                  ([f, h, conj(f), conj(h), g], 1), ([f, h, conj(f), h, g], 0)]
+        bad = conj(f)
+        bad[7] = (bad[7] + 1) % O.P
+        cases.append(([f, bad], 0))
+    cases.append(([[(1 << 406) % O.P] + [0] * 11], 1))  # one (Montgomery radix 2^406)
+    for fs, want in cases:
+        assert check(fs, 1) == want, (len(fs), want)
+        assert check(fs, 0) == want, (len(fs), want)
