@@ -86,18 +86,19 @@ __global__ void __launch_bounds__(64) k_h2c_wide(size_t B, const uint8_t* msgs, 
   sswu_w(K, uh, x, y, rare);
   const J2W P = iso_w(K, x, y, izero);
   const J2W Po{w2swap(P.x), w2swap(P.y), w2swap(P.z)};
-  const J2W Q = j2w_add(K, P, Po, exc);
-  const W2 cx = w2const(PSI_CX), cy = w2const(PSI_CY);
+  // Q = P0 + P1 (W2 layout, both halves), then the cofactor chains in F2 layout on half 0's Q
+  const J2F Q = j2f_of_j2w(j2w_add(K, P, Po, exc));
+  const uint32_t cx = wf_from_fp2(PSI_CX), cy = wf_from_fp2(PSI_CY);
   const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
-  const J2W M = j2w_mul_xabs(K, Q, exc);
-  const J2W npq = j2w_neg(K, j2w_psi(K, Q, cx, cy));
-  const J2W Ap = j2w_add(K, M, npq, exc);
-  J2W C = j2w_add(K, j2w_psi2(K, j2w_dbl(K, Q), c2x, c2y), npq, exc);
-  C = j2w_add(K, C, M, exc);
-  C = j2w_add(K, C, j2w_neg(K, Q), exc);
-  const J2W M2 = j2w_mul_xabs(K, Ap, exc);
-  const J2W Hj = j2w_add(K, C, M2, exc);
-  const G2A h = j2w_to_aff(K, Hj);
+  const J2F M = j2f_mul_xabs(K, Q, exc);
+  const J2F npq = j2f_neg(K, j2f_psi(K, Q, cx, cy));
+  const J2F Ap = j2f_add(K, M, npq, exc);
+  J2F C = j2f_add(K, j2f_psi2(j2f_dbl(K, Q), c2x, c2y), npq, exc);
+  C = j2f_add(K, C, M, exc);
+  C = j2f_add(K, C, j2f_neg(K, Q), exc);
+  const J2F M2 = j2f_mul_xabs(K, Ap, exc);
+  const J2F Hj = j2f_add(K, C, M2, exc);
+  const G2A h = j2f_to_aff(K, Hj);
   const int bad = (rare | izero | exc) ? 1 : 0;
   const int bad_any = __builtin_amdgcn_readlane(bad, 0) | __builtin_amdgcn_readlane(bad, 32);
   if (threadIdx.x == 0) {

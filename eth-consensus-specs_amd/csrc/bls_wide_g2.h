@@ -218,5 +218,96 @@ __device__ __forceinline__ G2A j2w_to_aff(const WKG& K, const J2W& p) {
   return r;
 }
 
+// ---- G2 Jacobian in F2 layout: one VGPR per coordinate (c0 in half 0, c1 in half 1) --------------------------
+// The same formulas, bounds and subtraction constants as J2W; an Fp2 product is one wdot2 per half instead of two
+// one after another, so the cofactor chains of hash_to_G2 (after the two halves' SSWU results are added) stop
+// computing everything twice.
+struct J2F {
+  uint32_t x, y, z;
+};
+// half 0's W2 value in F2 layout (c0 from half 0's c0 register, c1 from half 0's c1 register)
+__device__ __forceinline__ uint32_t wf_of_w2(W2 a) {
+  const uint32_t s1 = wswap(a.c1);
+  return whalf() ? s1 : a.c0;
+}
+__device__ __forceinline__ J2F j2f_of_j2w(const J2W& p) { return J2F{wf_of_w2(p.x), wf_of_w2(p.y), wf_of_w2(p.z)}; }
+// both coefficients zero (the same answer in both halves)
+__device__ __forceinline__ bool wf_is_zero(uint32_t v) { return w_is_zero(v) & w_is_zero(wswap(v)); }
+
+__device__ __forceinline__ J2F j2f_dbl(const WKG& K, const J2F& p) {
+  const uint32_t ks = K.k2048_2, kn = K.kneg;
+  const uint32_t A = wf_sqr(ks, p.x);
+  const uint32_t Bq = wf_sqr(ks, p.y);
+  const uint32_t C = wf_sqr(ks, Bq);
+  const uint32_t XB2 = wf_sqr(ks, wadd(p.x, Bq));
+  const uint32_t D = wmuls<2>(wsubk(K.k2, XB2, wadd(A, C)));
+  const uint32_t E = wmuls<3>(A);
+  J2F r;
+  r.x = wsubk(K.k1024, wf_sqr(ks, E), wmuls<2>(D));
+  const uint32_t DX = wsubk(K.k2048_2, D, r.x);
+  r.y = wsubk(K.k1, wf_mul(kn, E, DX), wmuls<8>(C));
+  r.z = wmuls<2>(wf_mul(kn, p.y, p.z));
+  return r;
+}
+
+__device__ __forceinline__ J2F j2f_add(const WKG& K, const J2F& p, const J2F& q, bool& exc) {
+  const uint32_t ks = K.k2048_2, kn = K.kneg;
+  const uint32_t z1z1 = wf_sqr(ks, p.z);
+  const uint32_t z2z2 = wf_sqr(ks, q.z);
+  const uint32_t u1 = wf_mul(kn, p.x, z2z2);
+  const uint32_t u2 = wf_mul(kn, q.x, z1z1);
+  const uint32_t s1 = wf_mul(kn, wf_mul(kn, p.y, q.z), z2z2);
+  const uint32_t s2 = wf_mul(kn, wf_mul(kn, q.y, p.z), z1z1);
+  const uint32_t h = wsubk(K.k256, u2, u1);
+  exc = exc | wf_is_zero(h) | wf_is_zero(p.z) | wf_is_zero(q.z);
+  const uint32_t rr = wmuls<2>(wsubk(K.k256, s2, s1));
+  const uint32_t i = wf_sqr(ks, wmuls<2>(h));
+  const uint32_t j = wf_mul(kn, h, i);
+  const uint32_t v = wf_mul(kn, u1, i);
+  J2F r;
+  r.x = wsubk(K.k512_2, wf_sqr(ks, rr), wadd(j, wmuls<2>(v)));
+  const uint32_t vx = wsubk(K.k1024, v, r.x);
+  r.y = wsubk(K.k512_2, wf_mul(kn, rr, vx), wmuls<2>(wf_mul(kn, s1, j)));
+  const uint32_t zz = wsubk(K.k2, wf_sqr(ks, wadd(p.z, q.z)), wadd(z1z1, z2z2));
+  r.z = wf_mul(kn, zz, h);
+  return r;
+}
+
+__device__ __forceinline__ J2F j2f_mul_xabs(const WKG& K, const J2F& p, bool& exc) {
+  J2F m = p;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    m = j2f_dbl(K, m);
+    if ((X_ABS >> b) & 1ull) m = j2f_add(K, m, p, exc);
+  }
+  return m;
+}
+__device__ __forceinline__ J2F j2f_neg(const WKG& K, const J2F& p) {
+  return J2F{p.x, wsubk(K.k1, 0u, wmul(p.y, K.one)), p.z};
+}
+// psi(P) = (conj(X) cx, conj(Y) cy, conj(Z)); cx, cy in F2 layout
+__device__ __forceinline__ J2F j2f_psi(const WKG& K, const J2F& p, uint32_t cx, uint32_t cy) {
+  const uint32_t zc = wmul(wf_conj(K.k2048_2, p.z), K.one);
+  return J2F{wf_mul(K.kneg, wf_conj(K.k2048_2, p.x), cx), wf_mul(K.kneg, wf_conj(K.k2048_2, p.y), cy), zc};
+}
+// psi^2(P) = (X c2x, Y c2y, Z) (c2x, c2y in Fp, both halves)
+__device__ __forceinline__ J2F j2f_psi2(const J2F& p, uint32_t c2x, uint32_t c2y) {
+  return J2F{wmul(p.x, c2x), wmul(p.y, c2y), p.z};
+}
+// Jacobian -> affine (x, y) canonical packed; the identity (Z = 0) -> inf
+__device__ __forceinline__ G2A j2f_to_aff(const WKG& K, const J2F& p) {
+  const uint32_t sq = wsqr(p.z);  // z0^2 | z1^2
+  const uint32_t nz = wadd(sq, wswap(sq));  // norm(Z) in both halves
+  const Fp nl = w_to_fp(nz);
+  G2A r{fp2_zero(), fp2_zero(), true};
+  const uint32_t ni = w_from_fp(fp_inv_sg_i(nl));
+  const uint32_t zi = wmul(wf_conj(K.k2048_2, p.z), ni);
+  const uint32_t zi2 = wf_mul(K.kneg, zi, zi);
+  const uint32_t zi3 = wf_mul(K.kneg, zi2, zi);
+  const Fp2 x = wf_to_fp2(wf_mul(K.kneg, p.x, zi2)), y = wf_to_fp2(wf_mul(K.kneg, p.y, zi3));
+  if (!fp_is_zero(nl)) r = G2A{x, y, false};
+  return r;
+}
+
 }  // namespace wide
 }  // namespace bls
