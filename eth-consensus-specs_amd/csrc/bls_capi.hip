@@ -70,7 +70,10 @@ struct Job {
 
 struct bls_ctx {
   int device = 0;
-  bool fe_wide = true;  // final checks on the six-wave kernel (k_fe_wide); BLS_FE_WIDE=0: the one-wave k_fe_check
+  // per-call final checks on the six-wave kernel (k_fe_wide, latency); BLS_FE_WIDE=0: the one-wave k_fe_check.
+  // Batch checks stay on k_fe_check: off their critical path, one wave leaves the CU to the pipeline (the A/B of
+  // profiles/r04m_fe_ab.txt: 1.92 M vs 1.84 M FAV/s with the six-wave kernel)
+  bool fe_wide = true;
   int njobs = 6;  // job slots with streams: BLS_FAV_JOBS_INIT (default 6, at most BLS_FAV_JOBS)
   Job jobs[BLS_FAV_JOBS];
   Job* j = &jobs[0];  // the job the current call works on
@@ -250,13 +253,13 @@ void prof_collect(bls_ctx* c) {
 
 // Final-exponentiation check of the product of f[0 .. n) on the context's FE
 // stream, after the current job's stream: 1 / 0.
-int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
+int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1, bool percall = false) {
   int* d_r;
   SCR(S_INT, 4, d_r);
   Job& J = *ctx->j;
   HIPCK(hipEventRecord(J.ev_fe, J.stream));
   HIPCK(hipStreamWaitEvent(ctx->fe_stream, J.ev_fe, 0));
-  if (ctx->fe_wide)
+  if (percall && ctx->fe_wide)
     PROF2(7, ctx->fe_stream, launch_fe_wide(ctx->fe_stream, f, n, d_r));
   else
     PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
@@ -497,7 +500,7 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   LK(launch_miller_wide(st, P, Q, nullptr, ok + n, 2, f + 2));
   int live = 0;
   HIPCK(hipMemcpyAsync(&live, ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-  const int fe = run_final_check(ctx, f + 2);  // orders after st
+  const int fe = run_final_check(ctx, f + 2, 1, true);  // orders after st
   if (fe < 0) return fe;
   HIPCK(hipStreamSynchronize(st));  // `live` is pageable host memory
   return (live && fe) ? 1 : 0;

@@ -335,14 +335,16 @@ __global__ void __launch_bounds__(64) k_sig_validate_wide(const uint8_t* sigs96,
         if (fp2_lex_largest(yl) != a_flag) y = w2neg(K1, y);
         y = w2red(K, y);
         bool exc = false;
-        const J2W M = j2w_mul_xabs(K, J2W{xm, y, W2{K.one, 0u}}, exc);
+        // the subgroup chain in F2 layout (bls_wide_g2.h J2F)
+        const uint32_t xf = wf_of_w2(xm), yf = wf_of_w2(y), kn = K.kneg;
+        const J2F M = j2f_mul_xabs(K, J2F{xf, yf, wf_from_fp2(fp2_one())}, exc);
         // psi(sigma) == -M:  conj(x) CX Z^2 == X,  conj(y) CY Z^3 == -Y,  Z != 0
-        const W2 zz = w2mulk(K, M.z, M.z);
-        const W2 px = w2mulk(K, w2mulk(K, w2conj(K1, xm), w2const(PSI_CX)), zz);
-        const W2 py = w2mulk(K, w2mulk(K, w2conj(K1, y), w2const(PSI_CY)), w2mulk(K, zz, M.z));
-        const bool zx = w2_is_zero(w2subk(K.k2048_2, px, M.x));  // M.x < 1028p (the chain ends on a doubling)
-        const bool zy = w2_is_zero(w2add(py, M.y));
-        const bool zz0 = w2_is_zero(M.z);
+        const uint32_t zz = wf_mul(kn, M.z, M.z);
+        const uint32_t px = wf_mul(kn, wf_mul(kn, wf_conj(K.k1, xf), wf_from_fp2(PSI_CX)), zz);
+        const uint32_t py = wf_mul(kn, wf_mul(kn, wf_conj(K.k1, yf), wf_from_fp2(PSI_CY)), wf_mul(kn, zz, M.z));
+        const bool zx = wf_is_zero(wsubk(K.k2048_2, px, M.x));  // M.x < 1028p (the chain ends on a doubling)
+        const bool zy = wf_is_zero(wadd(py, M.y));
+        const bool zz0 = wf_is_zero(M.z);
         if (!exc && !zz0 && zx && zy) {
           v = 1;
           s = G2A{w2_to_fp2(xm), w2_to_fp2(y), false};
