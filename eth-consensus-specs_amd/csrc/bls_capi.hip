@@ -70,10 +70,6 @@ struct Job {
 
 struct bls_ctx {
   int device = 0;
-  // per-call final checks on the six-wave kernel (k_fe_wide, latency); BLS_FE_WIDE=0: the one-wave k_fe_check.
-  // Batch checks stay on k_fe_check: off their critical path, one wave leaves the CU to the pipeline (the A/B of
-  // profiles/r04m_fe_ab.txt: 1.92 M vs 1.84 M FAV/s with the six-wave kernel)
-  bool fe_wide = true;
   int njobs = 6;  // job slots with streams: BLS_FAV_JOBS_INIT (default 6, at most BLS_FAV_JOBS)
   Job jobs[BLS_FAV_JOBS];
   Job* j = &jobs[0];  // the job the current call works on
@@ -259,7 +255,9 @@ int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1, bool percall = false
   Job& J = *ctx->j;
   HIPCK(hipEventRecord(J.ev_fe, J.stream));
   HIPCK(hipStreamWaitEvent(ctx->fe_stream, J.ev_fe, 0));
-  if (percall && ctx->fe_wide)
+  // per-call checks on the six-wave k_fe_wide (latency); batch checks on the one-wave k_fe_check, which leaves the
+  // CU to the other jobs (profiles/r04m_fe_ab.txt: 1.92 M vs 1.84 M FAV/s with every check six-wave)
+  if (percall)
     PROF2(7, ctx->fe_stream, launch_fe_wide(ctx->fe_stream, f, n, d_r));
   else
     PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
@@ -383,7 +381,6 @@ int bls_ctx_create(int device, bls_ctx** out) {
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   // All job streams are created here, before any kernel runs (streams created
   // later, between launches, were measured to hit HSA_STATUS_ERROR_OUT_OF_RESOURCES).
-  if (const char* v = getenv("BLS_FE_WIDE")) c->fe_wide = atoi(v) != 0;
   if (const char* v = getenv("BLS_FAV_JOBS_INIT")) c->njobs = atoi(v) < 1 ? 1 : atoi(v) > BLS_FAV_JOBS ? BLS_FAV_JOBS : atoi(v);
   for (int k = 0; k < c->njobs; ++k) {
     if (!job_init(c->jobs[k], prio_hi)) {
@@ -1031,7 +1028,9 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     LK(launch_msm(st3, B, gstat, dstat, rsc, sig, msmu, msmf, saff));
     hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, rP + B);
     LK(hipGetLastError());
-    LK(launch_miller_wave(st3, rP + B, saff, nullptr, 1, f + B + 1));
+    // the one pair (-G1, S) on the fused wide Miller kernel (bls_wide.hip k_miller_wide): the MSM-side chain is
+    // latency, one wave per step of the lane kernel was ~2.1 ms of it
+    LK(launch_miller_wide(st3, rP + B, saff, nullptr, nullptr, 1, f + B + 1));
   }
   HIPCK(hipEventRecord(ctx->j->ev_msm, st3));
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_sig, 0));

@@ -101,6 +101,8 @@ hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t 
 hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L);
 hipError_t launch_facc_wide(hipStream_t st, const uint32_t* L, int npairs, Fp12* out);
 size_t lines_wide_u32(size_t n);
+// S = sum_b 2^b U_b of the MSM's 64 bit-sums (packed projective, bls_msm.hip) on one 16-wave workgroup
+hipError_t launch_msm_weighted_wide(hipStream_t st, const Fp* U, G2A* out);
 // the whole Miller loop of npairs <= 2 pairs on one workgroup (line waves + six f waves): out = f (tower Fp12);
 // ok0 / ok1 (nullable): pair 0 / 1 runs with constant lines unless *okp
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,

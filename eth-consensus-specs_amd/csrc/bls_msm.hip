@@ -6,13 +6,15 @@
 //   k_msm_count, k_msm_scan, k_msm_scatter   the sort
 //   k_msm_bucketc   each bucket's points summed in MSM_C = 8 strided chunks,
 //                   one lane pair per chunk (~5 mixed additions each; 16,384
-//                   chunks = 512 waves, the point loads one step ahead)
+//                   chunks = 512 waves, the point loads one step ahead), the
+//                   chunks then folded into the bucket sum B_{w,d} in LDS
 //   k_msm_usum      U_b = sum_{d : bit k of d} B_{w,d}  (b = 8w + k): one
-//                   workgroup per b, each lane pair sums its digit's 8 chunks,
-//                   then a 7-level tree through LDS
-//   k_msm_weighted  S = sum_b 2^b U_b: a 6-level tree through LDS pairing
-//                   node j with j + s and weighting it by 2^s (63 doublings on
-//                   the longest chain), then S -> affine
+//                   workgroup per b, a 7-level LDS tree over its 128 digits'
+//                   bucket sums (a 16-wave wide-arithmetic variant measured
+//                   C2 -4 %: profiles/r04o_usum_ab.txt)
+//   k_msm_weighted_wide  S = sum_b 2^b U_b in wavefront-cooperative arithmetic,
+//                   one 16-wave workgroup (bls_msm_wide.hip; the lane-pair tree
+//                   it replaces took ~1.6 ms of latency per batch), S -> affine
 // ~8 additions per signature instead of a 64-step double-and-add; the chain
 // runs on its own high-priority stream beside the Miller loops of the
 // (r_i apk_i, H_i) pairs.  (The previous form ran one lane pair per bucket --
@@ -20,9 +22,7 @@
 // launches: ~6.8 ms per C2 batch.)
 #include "bls_kernels.h"
 #include "bls_pp_lane.h"
-#include "bls_fp_inv.h"
 
-#include <stdlib.h>
 
 namespace bls {
 
@@ -94,12 +94,6 @@ __device__ __forceinline__ void p2_store(Fp* o, const P2& p, bool hi) {  // sele
   d[1] = fp_select(hi, p.z.c0, p.x.c1);
   d[2] = fp_select(hi, p.z.c1, p.y.c0);
 }
-// 1 / (a0 + a1 i) = (a0 - a1 i) / (a0^2 + a1^2) with the inline Fp inverse (an out-of-line call here cost a
-// 960-B private segment on the job's stream)
-__device__ __forceinline__ Fp2 fp2_inv_inline(const Fp2& a) {
-  const Fp ni = fp_inv_sg_i(fp_add(fp_sqr_i(a.c0), fp_sqr_i(a.c1)));
-  return Fp2{fp_mul_i(a.c0, ni), fp_neg(fp_mul_i(a.c1, ni))};
-}
 __device__ __forceinline__ P2 p2_load(const Fp* in) {
   return P2{Fp2{in[0], in[1]}, Fp2{in[2], in[3]}, Fp2{in[4], in[5]}};
 }
@@ -126,10 +120,21 @@ __global__ void __launch_bounds__(64) k_msm_bucketc(const uint32_t* off, const u
     li = k + 2 * MSM_C < end ? lst[k + 2 * MSM_C] : 0u;
     R = pp2_add_aff(R, cq.x, cq.y, hi);
   }
-  p2_store(csum + (size_t)pi * 6, R, hi);
+  // the bucket's MSM_C chunk sums (lane pairs 8 b' .. 8 b' + 7 of this wave) folded by a 3-level LDS tree, so the
+  // U sums read one point per bucket instead of re-adding its chunks once per set bit of the digit
+  __shared__ Fp sm[32 * 6];
+  const int lp = threadIdx.x >> 1;  // lane pair in the wave
+#pragma unroll 1
+  for (int s = MSM_C / 2; s >= 1; s >>= 1) {
+    if (c >= s && c < 2 * s) p2_store(sm + 6 * (lp - s), R, hi);
+    __syncthreads();
+    if (c < s) R = pp2_add(R, p2_load(sm + 6 * lp), hi);
+    __syncthreads();
+  }
+  if (c == 0) p2_store(csum + (size_t)b * 6, R, hi);
 }
 
-// U_b for b = blockIdx.x (w = b / 8, bit k = b % 8): lane pair j sums the MSM_C chunks of digit d_j (the j-th
+// U_b for b = blockIdx.x (w = b / 8, bit k = b % 8): lane pair j reads the bucket sum of digit d_j (the j-th
 // digit with bit k set), then the 128 pair sums go through a 7-level LDS tree
 __global__ void __launch_bounds__(256) k_msm_usum(const Fp* csum, Fp* U) {
   __shared__ Fp sm[128 * 6];
@@ -137,10 +142,7 @@ __global__ void __launch_bounds__(256) k_msm_usum(const Fp* csum, Fp* U) {
   const int j = threadIdx.x >> 1;
   const bool hi = (threadIdx.x & 1) != 0;
   const int d = ((j >> kb) << (kb + 1)) | (1 << kb) | (j & ((1 << kb) - 1));
-  const Fp* in = csum + (size_t)(w * 256 + d) * MSM_C * 6;
-  P2 R = p2_load(in);
-#pragma unroll 1
-  for (int c = 1; c < MSM_C; ++c) R = pp2_add(R, p2_load(in + 6 * c), hi);
+  P2 R = p2_load(csum + (size_t)(w * 256 + d) * 6);  // the bucket sum B_{w,d}
 #pragma unroll 1
   for (int s = 64; s >= 1; s >>= 1) {
     if (j >= s && j < 2 * s) p2_store(sm + 6 * (j - s), R, hi);
@@ -149,39 +151,6 @@ __global__ void __launch_bounds__(256) k_msm_usum(const Fp* csum, Fp* U) {
     __syncthreads();
   }
   if (j == 0) p2_store(U + 6 * b, R, hi);
-}
-
-// S = sum_b 2^b U_b and its affine form: node j (< s) adds 2^s node_{j+s}, s = 32, 16, ..., 1 (node j of the
-// first level reads U_j and U_{j+32} from HBM); one workgroup of 32 lane pairs
-__global__ void __launch_bounds__(64) k_msm_weighted(const Fp* U, G2A* out) {
-  __shared__ Fp sm[32 * 6];
-  const int j = threadIdx.x >> 1;
-  const bool hi = (threadIdx.x & 1) != 0;
-  P2 R = p2_load(U + 6 * j);
-  P2 Bp = p2_load(U + 6 * (j + 32));
-#pragma unroll 1
-  for (int i = 0; i < 32; ++i) Bp = pp2_dbl(Bp, hi);
-  R = pp2_add(R, Bp, hi);
-#pragma unroll 1
-  for (int s = 16; s >= 1; s >>= 1) {
-    if (j >= s && j < 2 * s) p2_store(sm + 6 * (j - s), R, hi);
-    __syncthreads();
-    if (j < s) {
-      Bp = p2_load(sm + 6 * j);
-#pragma unroll 1
-      for (int i = 0; i < s; ++i) Bp = pp2_dbl(Bp, hi);
-      R = pp2_add(R, Bp, hi);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {  // (X : Y : Z) -> (X / Z, Y / Z); Z = 0 is the identity
-    G2A r;
-    r.inf = fp2_is_zero(R.z);
-    const Fp2 zi = fp2_inv_inline(R.z);
-    r.x = r.inf ? fp2_zero() : f2mul(R.x, zi);
-    r.y = r.inf ? fp2_zero() : f2mul(R.y, zi);
-    *out = r;
-  }
 }
 
 // Scratch: cnt[MSM_NB] | off[MSM_NB + 1] | cur[MSM_NB] (u32), lst[8 B] (u32);
@@ -214,8 +183,7 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_usum, dim3(64), dim3(256), 0, st, csum, U);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_weighted, dim3(1), dim3(64), 0, st, U, out);
-  return hipGetLastError();
+  return launch_msm_weighted_wide(st, U, out);
 }
 
 }  // namespace bls
