@@ -293,3 +293,14 @@ def test_resident_batch_chunked(batch, registry):
     finally:
         rbc.free()
         rb1.free()
+
+
+@pytest.mark.parametrize("B", [1, 2, 5])
+def test_fav_small_batch_msm_identities(batch, registry, B):
+    """Batches of 1, 2 and 5 items: most of the MSM's 64 bit-sums U_b are the identity (only the bits the few RLC
+    scalars set), so the wide weighted sum (k_msm_weighted_wide, complete projective formulas) must carry
+    identities through doublings and additions; a wrong S would fail the batch check and show as fallback work."""
+    idx, offs, msgs, sigs = _make_batch(batch, B, 8, seed=40 + B)
+    out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+    assert out.all()
+    assert batch.fallback_stats() == (0, 0)
