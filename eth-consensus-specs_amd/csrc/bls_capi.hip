@@ -91,6 +91,8 @@ struct bls_ctx {
   // the lane kernels' flags; null in every product use
   int* force_fb = nullptr;
   size_t force_fb_n = 0;
+  uint8_t* pc_stage = nullptr;  // pinned staging of a per-call's inputs: one DMA instead of four pageable copies
+  size_t pc_stage_cap = 0;
   // multi-GPU exchange of FAV partials (bls_comm_*): one RCCL communicator
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
@@ -305,6 +307,10 @@ int h2c_fallback(bls_ctx* ctx, hipStream_t st, size_t B, const uint8_t* msgs, co
   return 0;
 }
 
+__global__ void k_copy_int(const int* src, int* dst) {
+  if (threadIdx.x == 0) *dst = *src;
+}
+
 __global__ void k_set_neg_g1(G1A* p) {
   if (threadIdx.x || blockIdx.x) return;
   G1A g = g1_generator();
@@ -414,6 +420,7 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   }
   if (ctx->reg) (void)hipFree(ctx->reg);
   if (ctx->force_fb) (void)hipFree(ctx->force_fb);
+  if (ctx->pc_stage) (void)hipHostFree(ctx->pc_stage);
   delete ctx;
 }
 
@@ -455,8 +462,10 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   Fp12* f;
   uint64_t* d_offs;
   const size_t in_bytes = 48 * n + 96 + msg_len;
-  SCR(S_IN0, in_bytes + 16, d_in);
-  SCR(S_OFFS, 2, d_offs);
+  const size_t offs_at = (in_bytes + 7) & ~(size_t)7;  // the two message offsets after the inputs, 8-B aligned
+  const size_t total = offs_at + 16;
+  SCR(S_IN0, total, d_in);
+  d_offs = reinterpret_cast<uint64_t*>(d_in + offs_at);
   SCR(S_G1A, n, keys);
   SCR(S_OK, n + 2, ok);  // key verdicts | sig verdict | live
   SCR(S_PC_P, 2, P);  // P[0] apk, P[1] -G1 (k_percall_pairs)
@@ -471,10 +480,18 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   uint8_t* d_sig = d_in + 48 * n;
   uint8_t* d_msg = d_in + 48 * n + 96;
   const uint64_t offs[2] = {0, msg_len};
-  CK(h2d(ctx, d_pk, pks48, 48 * n));
-  CK(h2d(ctx, d_sig, sig96, 96));
-  CK(h2d(ctx, d_msg, msg, msg_len));
-  CK(h2d(ctx, d_offs, offs, sizeof offs));
+  if (ctx->pc_stage_cap < total) {  // grows to the largest call seen; the previous call has synchronised
+    if (ctx->pc_stage) HIPCK(hipHostFree(ctx->pc_stage));
+    ctx->pc_stage = nullptr;
+    ctx->pc_stage_cap = 0;
+    HIPCK(hipHostMalloc((void**)&ctx->pc_stage, total, hipHostMallocDefault));
+    ctx->pc_stage_cap = total;
+  }
+  memcpy(ctx->pc_stage, pks48, 48 * n);
+  memcpy(ctx->pc_stage + 48 * n, sig96, 96);
+  if (msg_len) memcpy(ctx->pc_stage + 48 * n + 96, msg, msg_len);
+  memcpy(ctx->pc_stage + offs_at, offs, sizeof offs);
+  CK(h2d(ctx, d_in, ctx->pc_stage, total));
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
@@ -495,12 +512,15 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   // both pairs' Miller loop on one workgroup: (apk, H) -- rejected inputs are identities there, `live` decides --
   // and (-G1, sigma), constant lines for a rejected signature
   LK(launch_miller_wide(st, P, Q, nullptr, ok + n, 2, f + 2));
-  int live = 0;
-  HIPCK(hipMemcpyAsync(&live, ok + n + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-  const int fe = run_final_check(ctx, f + 2, 1, true);  // orders after st
-  if (fe < 0) return fe;
-  HIPCK(hipStreamSynchronize(st));  // `live` is pageable host memory
-  return (live && fe) ? 1 : 0;
+  // the six-wave final check on the same stream, then both verdict words in one copy (FE | live) and one sync
+  PROF2(7, st, launch_fe_wide(st, f + 2, 1, d_r));
+  hipLaunchKernelGGL(k_copy_int, dim3(1), dim3(64), 0, st, ok + n + 1, d_r + 1);
+  LK(hipGetLastError());
+  int res[2] = {0, 0};
+  HIPCK(hipMemcpyAsync(ctx->pc_stage, d_r, sizeof res, hipMemcpyDeviceToHost, st));
+  HIPCK(hipStreamSynchronize(st));
+  memcpy(res, ctx->pc_stage, sizeof res);
+  return (res[0] && res[1]) ? 1 : 0;
 }
 
 int bls_verify(bls_ctx* ctx, const uint8_t* pk48, const uint8_t* msg, size_t msg_len, const uint8_t* sig96) {
