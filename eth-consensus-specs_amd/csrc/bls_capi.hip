@@ -549,50 +549,64 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
     offs[i + 1] = offs[i] + msg_lens[i];
   }
   if (offs[n] && !msgs) return BLS_E_ARG;
-  G1A* P;
-  int* ok;
-  int v = validate_pks(ctx, pks48, n, &P, &ok);
-  if (v <= 0) return v;
+  // three streams as verify_percall: the signature's decode + subgroup check (stream3) and the n hashes
+  // (stream2) run beside the keys' validation (stream1, which synchronises for the verdicts), the Miller loops
+  // join them; a rejected signature is reported through its verdict word next to the FE result
+  Job& J = *ctx->j;
+  hipStream_t st = J.stream, st2 = J.stream2, st3 = J.stream3;
   uint8_t *d_sig, *d_msgs;
   uint64_t* d_offs;
   G2A* Q;
-  int* d_sok;
+  int* d_w;
   Fp12 *f, *ft, *fo;
+  Fd* d_hf;
+  int* d_flag;
   SCR(S_IN1, 96, d_sig);
   SCR(S_IN2, offs[n], d_msgs);
   SCR(S_OFFS, n + 1, d_offs);
   SCR(S_G2A, n + 1, Q);
-  SCR(S_INT, 4, d_sok);
+  SCR(S_INT, 4, d_w);  // sig verdict | FE verdict
   SCR(S_F, n + 1, f);
   SCR(S_F_T, (n + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
+  SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
+  SCR(S_AV_FLAG, n, d_flag);
   CK(h2d(ctx, d_sig, sig96, 96));
-  LK(launch_sig_validate(ctx->j->stream, d_sig, 1, Q + n, d_sok));
-  int sok = 0;
-  CK(d2h(ctx, &sok, d_sok, sizeof sok));
-  if (!sok) return 0;
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
-  {
-    Fd* d_hf;
-    int* d_flag;
-    SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
-    SCR(S_AV_FLAG, n, d_flag);
-    bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
-    for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
-    if (n <= WIDE_H2C_MAX)  // a few messages: one wave each, lower latency than the lane kernels' chains
-      LK(launch_h2c_wide(ctx->j->stream, n, d_msgs, m32 ? nullptr : d_offs, Q, d_flag));
-    else if (m32)
-      LK(launch_h2c(ctx->j->stream, n, d_msgs, nullptr, d_hf, Q, d_flag));
-    else
-      LK(launch_h2c_msgs(ctx->j->stream, n, d_msgs, d_offs, d_hf, Q, d_flag));
-    CK(h2c_fallback(ctx, ctx->j->stream, n, d_msgs, m32 ? nullptr : d_offs, d_flag, Q));
+  HIPCK(hipEventRecord(J.ev_fork, st));
+  HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
+  HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
+  LK(launch_sig_validate_wide(st3, d_sig, 1, Q + n, d_w));
+  HIPCK(hipEventRecord(J.ev_sig, st3));
+  bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
+  for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
+  if (n <= WIDE_H2C_MAX)  // a few messages: one wave each, lower latency than the lane kernels' chains
+    LK(launch_h2c_wide(st2, n, d_msgs, m32 ? nullptr : d_offs, Q, d_flag));
+  else if (m32)
+    LK(launch_h2c(st2, n, d_msgs, nullptr, d_hf, Q, d_flag));
+  else
+    LK(launch_h2c_msgs(st2, n, d_msgs, d_offs, d_hf, Q, d_flag));
+  CK(h2c_fallback(ctx, st2, n, d_msgs, m32 ? nullptr : d_offs, d_flag, Q));
+  HIPCK(hipEventRecord(J.ev_join, st2));
+  G1A* P;
+  int* ok;
+  const int v = validate_pks(ctx, pks48, n, &P, &ok);  // synchronises stream1
+  if (v <= 0) {
+    HIPCK(hipStreamSynchronize(st2));  // the scratch of the side streams is reused by the next call
+    HIPCK(hipStreamSynchronize(st3));
+    return v;
   }
-  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ctx->j->stream, P + n);
+  HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
+  HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
+  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st, P + n);
   LK(hipGetLastError());
-  LK(launch_miller_wave(ctx->j->stream, P, Q, nullptr, n + 1, f));
-  LK(launch_fp12_prod_vm(ctx->j->stream, f, n + 1, ft, fo));
-  return run_final_check(ctx, fo);
+  LK(launch_miller_wave(st, P, Q, nullptr, n + 1, f));  // a rejected signature is the identity there
+  LK(launch_fp12_prod_vm(st, f, n + 1, ft, fo));
+  PROF2(7, st, launch_fe_wide(st, fo, 1, d_w + 1));
+  int w[2] = {0, 0};
+  CK(d2h(ctx, w, d_w, sizeof w));
+  return (w[0] && w[1]) ? 1 : 0;
 }
 
 int bls_aggregate(bls_ctx* ctx, const uint8_t* sigs96, size_t n, uint8_t* out96) {
