@@ -1,11 +1,10 @@
-// k_fe_wide: the final-exponentiation check with the hard part in wavefront-cooperative arithmetic (bls_wide.h,
-// F2 layout) on six waves -- the per-call path's check.  Same schedule, same answer as k_fe_check
+// k_fe_wide: the final-exponentiation check in wavefront-cooperative arithmetic (bls_wide.h, F2 layout) on six
+// waves, easy and hard part -- the per-call path's check.  Same schedule, same answer as k_fe_check
 // (bls_fe.hip), which stays the batch / bisection check.
 #include "bls_kernels.h"
 #include "bls_lane.h"
 #include "bls_wide.h"
 #include "bls_wide_g2.h"
-#include "bls_fe.h"
 
 namespace bls {
 
@@ -94,6 +93,52 @@ struct FeWide {
     wf_mac_fp(acc, ld(a, k), g2);
     put(d, wredc(acc), d == a);
   }
+  // easy part: bank 0 = f on entry, t = f^((p^6 - 1)(p^2 + 1)) on exit (banks 1 .. 5 temporaries):
+  //   g = conj(f), N = f g in Fp6 (the even coefficients n0, n2, n4 = Fp6 coefficients of v^0, v^1, v^2),
+  //   N^-1 = (t0, t1, t2) / d with t0 = n0^2 - xi n2 n4, t1 = xi n4^2 - n0 n2, t2 = n2^2 - n0 n4,
+  //   d = n0 t0 + xi (n4 t1 + n2 t2) (one Fp2 inversion: conj(d) / norm(d), the Fp inverse lane-local),
+  //   f^(p^6 - 1) = g^2 N^-1, then t = (f^(p^6 - 1))^(p^2) f^(p^6 - 1)
+  __device__ void easy(uint32_t g2) {
+    const uint32_t kn = K.kneg;
+    conj(0, 1);
+    mul(0, 1, 2);
+    {
+      const uint32_t n0 = ld(2, 0), n2 = ld(2, 2), n4 = ld(2, 4);
+      uint64_t acc = 0;
+      if (k == 0) {
+        wf_mac(acc, kn, n0, n0);
+        wf_mac(acc, kn, wsubk(K.k1024, 0u, xi(n2)), n4);
+      } else if (k == 2) {
+        wf_mac(acc, kn, xi(n4), n4);
+        wf_mac(acc, kn, wsubk(K.k1, 0u, n0), n2);
+      } else if (k == 4) {
+        wf_mac(acc, kn, n2, n2);
+        wf_mac(acc, kn, wsubk(K.k1, 0u, n0), n4);
+      }
+      put(3, (k & 1) ? 0u : wredc(acc), false);
+    }
+    if (k == 0) {
+      uint64_t acc = 0;
+      wf_mac(acc, kn, ld(2, 0), ld(3, 0));
+      wf_mac(acc, kn, xi(ld(2, 4)), ld(3, 2));
+      wf_mac(acc, kn, xi(ld(2, 2)), ld(3, 4));
+      const uint32_t d = wredc(acc);
+      const uint32_t sq = wsqr(d);
+      const Fp nl = w_to_fp(wadd(sq, wswap(sq)));  // norm(d) in both halves
+      const uint32_t ni = w_from_fp(fp_inv_sg_i(nl));
+      B[(4 * 6 + 0) * 64 + lane] = wmul(wf_conj(K.k1, d), ni);
+    }
+    __syncthreads();
+    {
+      uint64_t acc = 0;
+      wf_mac(acc, kn, ld(3, k), ld(4, 0));  // odd k: a zero coefficient
+      put(5, wredc(acc), false);
+    }
+    mul(1, 1, 2);
+    mul(2, 5, 0);  // f^(p^6 - 1)
+    frob2(0, 1, g2);
+    mul(1, 0, 0);
+  }
   // dst = src^x = conj(src^|x|): the chain ping-pongs between dst and tmp so each step has one barrier
   __device__ void powx(int src, int dst, int tmp) {
     int acc = src, o = dst;
@@ -112,21 +157,6 @@ struct FeWide {
   }
 };
 
-// the easy part on wave 0 (bls_fe.h executor), barriers kept by all six waves
-struct FeEasy : FeOps<FeEasy> {
-  FeSlot* s;
-  int lane;
-  bool active;
-  template <int KIND, int NX, int NY>
-  __device__ void ph(int phase, int a, int b, int d) {
-    if (active) {
-      const FeDesc<NX, NY> w = fe_desc<NX, NY>(phase, lane);
-      fe_lane<KIND, NX, NY>(s, w.w, a, b, d);
-    }
-    __syncthreads();
-  }
-};
-
 __global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const uint32_t* sel, int* out, uint64_t* ts) {
   int nts = 0;
   auto stamp = [&]() {
@@ -134,7 +164,6 @@ __global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const u
     nts++;
   };
   stamp();
-  __shared__ FeSlot s[FE_NSLOT];
   __shared__ uint32_t B[7 * 6 * 64];
   __shared__ int bad;
   const int lane = wlane(), k = (int)(threadIdx.x >> 6);
@@ -142,30 +171,7 @@ __global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const u
     fin += sel[blockIdx.x];
     out += blockIdx.x;
   }
-  if (k == 0) {
-    fe_load_consts(s, lane, 64);
-    if (lane == 0) {
-      bad = 0;
-      fe_st(s, FE_ABS_BASE + FE_CS, fq_zero());
-    }
-  }
-  FeEasy ex;
-  ex.s = s;
-  ex.lane = lane;
-  ex.active = k == 0;
-  __syncthreads();
-  for (int i = 0; i < n; i++) {
-    if (k == 0 && lane < 12) fe_st(s, 12 * (i ? 1 : 0) + lane, fq_unpack(reinterpret_cast<const Fp*>(fin + i)[lane]));
-    __syncthreads();
-    if (i) ex.mul(0, 1, 0);
-  }
-  stamp();
-  ex.easy(0, 2);
-  ex.easy_back(2, 0);
-  ex.frob2(0, 1);
-  ex.mul(1, 0, 0);  // bank 0 = t
-  stamp();
-  // t -> F2 layout: w^k is the tower Fp2 (k & 1) * 3 + (k >> 1), Fp slots 2 t, 2 t + 1
+  if (threadIdx.x == 0) bad = 0;
   FeWide W;
   W.B = B;
   W.k = k;
@@ -173,14 +179,24 @@ __global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const u
   W.K = wkg_init();
   W.two = wmuls<2>(W.K.one);
   W.mtwo = wnorm(W.K.k1 - W.two);
-  {
-    const int tp = (k & 1) * 3 + (k >> 1);
-    const int j = lane & 15;
-    const uint32_t dgt = j < 14 ? s[2 * tp + (lane >> 5)].d[j] : 0u;
-    B[(0 * 6 + k) * 64 + lane] = wmul(dgt, W.K.one);  // N-form digits -> W form, below 1.1 p
+  // the partials in F2 layout (w^k is the tower Fp2 (k & 1) * 3 + (k >> 1)), multiplied up in bank 0
+  const int tp = (k & 1) * 3 + (k >> 1);
+#pragma unroll 1
+  for (int i = 0; i < n; i++) {
+    const Fp* fp = reinterpret_cast<const Fp*>(fin + i);
+    const uint32_t v = wf_from_fp2(Fp2{fp[2 * tp], fp[2 * tp + 1]});
+    if (i == 0) {
+      B[(0 * 6 + k) * 64 + lane] = v;
+      __syncthreads();
+    } else {
+      W.put(1, v, false);
+      W.mul(0, 1, 0);
+    }
   }
-  __syncthreads();
+  stamp();
   const uint32_t wg1 = wf_from_fp2(FE_W_G1[k]), wg2 = w_from_fp(FE_W_G2[k].c0);
+  W.easy(wg2);  // bank 0 = t
+  stamp();
   // hard part, bls_fe.h fe_schedule's order (banks 0..5)
   W.powx(0, 1, 6);      // 1 = t^x
   stamp();
