@@ -70,7 +70,7 @@ struct Job {
 
 struct bls_ctx {
   int device = 0;
-  int njobs = 6;  // job slots with streams: BLS_FAV_JOBS_INIT (default 6, at most BLS_FAV_JOBS)
+  int njobs = 7;  // job slots with streams: BLS_FAV_JOBS_INIT (default 7, at most BLS_FAV_JOBS)
   Job jobs[BLS_FAV_JOBS];
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct bls_ctx bls_ctx;
 
-/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 6) get streams. */
+/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 7) get streams. */
 #define BLS_FAV_JOBS 8
 
 /* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
