@@ -9,9 +9,9 @@
 //                   chunks = 512 waves, the point loads one step ahead), the
 //                   chunks then folded into the bucket sum B_{w,d} in LDS
 //   k_msm_usum      U_b = sum_{d : bit k of d} B_{w,d}  (b = 8w + k): one
-//                   workgroup per b, a 7-level LDS tree over its 128 digits'
-//                   bucket sums (a 16-wave wide-arithmetic variant measured
-//                   C2 -4 %: profiles/r04o_usum_ab.txt)
+//                   wave per b, 32 lane pairs adding 4 bucket sums each, then a
+//                   5-level LDS tree (a 16-wave wide-arithmetic variant
+//                   measured C2 -4 %: profiles/r04o_usum_ab.txt)
 //   k_msm_weighted_wide  S = sum_b 2^b U_b in wavefront-cooperative arithmetic,
 //                   one 16-wave workgroup (bls_msm_wide.hip; the lane-pair tree
 //                   it replaces took ~1.6 ms of latency per batch), S -> affine
@@ -134,17 +134,25 @@ __global__ void __launch_bounds__(64) k_msm_bucketc(const uint32_t* off, const u
   if (c == 0) p2_store(csum + (size_t)b * 6, R, hi);
 }
 
-// U_b for b = blockIdx.x (w = b / 8, bit k = b % 8): lane pair j reads the bucket sum of digit d_j (the j-th
-// digit with bit k set), then the 128 pair sums go through a 7-level LDS tree
-__global__ void __launch_bounds__(256) k_msm_usum(const Fp* csum, Fp* U) {
-  __shared__ Fp sm[128 * 6];
+// U_b for b = blockIdx.x (w = b / 8, bit k = b % 8): one wave of 32 lane pairs; pair j adds the bucket sums of
+// the digits d_j, d_{j+32}, d_{j+64}, d_{j+96} (d_i = the i-th digit with bit k set), then a 5-level LDS tree.
+// (128 pairs over four waves with a 7-level tree ran one addition shorter but held 4x the waves at barriers:
+// 16 % -> 9 % of a C3 epoch's wave time after the bucket fold, profiles/r04n2_c3_timeline.txt.)
+constexpr int USUM_PAIRS = 32;
+__global__ void __launch_bounds__(64) k_msm_usum(const Fp* csum, Fp* U) {
+  __shared__ Fp sm[(USUM_PAIRS / 2) * 6];
   const int b = blockIdx.x, w = b >> 3, kb = b & 7;
   const int j = threadIdx.x >> 1;
   const bool hi = (threadIdx.x & 1) != 0;
-  const int d = ((j >> kb) << (kb + 1)) | (1 << kb) | (j & ((1 << kb) - 1));
-  P2 R = p2_load(csum + (size_t)(w * 256 + d) * 6);  // the bucket sum B_{w,d}
+  auto bucket = [&](int i) {
+    const int d = ((i >> kb) << (kb + 1)) | (1 << kb) | (i & ((1 << kb) - 1));
+    return csum + (size_t)(w * 256 + d) * 6;
+  };
+  P2 R = p2_load(bucket(j));
 #pragma unroll 1
-  for (int s = 64; s >= 1; s >>= 1) {
+  for (int t = 1; t < 128 / USUM_PAIRS; ++t) R = pp2_add(R, p2_load(bucket(j + USUM_PAIRS * t)), hi);
+#pragma unroll 1
+  for (int s = USUM_PAIRS / 2; s >= 1; s >>= 1) {
     if (j >= s && j < 2 * s) p2_store(sm + 6 * (j - s), R, hi);
     __syncthreads();
     if (j < s) R = pp2_add(R, p2_load(sm + 6 * j), hi);
@@ -181,7 +189,7 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   }
   hipLaunchKernelGGL(k_msm_bucketc, dim3(2 * MSM_NB * MSM_C / 64), dim3(64), 0, st, off, lst, sig, csum);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_usum, dim3(64), dim3(256), 0, st, csum, U);
+  hipLaunchKernelGGL(k_msm_usum, dim3(64), dim3(2 * USUM_PAIRS), 0, st, csum, U);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return launch_msm_weighted_wide(st, U, out);
 }
