@@ -117,9 +117,18 @@ BATCH_OPS = 9268 * FME_OPS  # shared per batch: 63 Fp12 squarings x 36 + final e
 
 # ------------------------------------------------------------------ workloads --
 def shard_bounds(total: int, rank: int, world: int) -> tuple[int, int]:
+    """C4: contiguous equal blocks of single-key Verify items (bls_mi355x.dist.shard_bounds)."""
     base, extra = divmod(total, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+def shard_bounds_by_work(offsets, rank: int, world: int) -> tuple[int, int]:
+    """C2 / C3 / C5: contiguous blocks of aggregates balanced by work (pubkeys + the per-aggregate constant;
+    bls_mi355x.dist.shard_bounds_by_work)."""
+    from bls_mi355x.dist import shard_bounds_by_work as f
+
+    return f(offsets, rank, world)
 
 
 def _msg(tag: bytes, seed: int, j: int) -> bytes:
@@ -155,7 +164,7 @@ def c3_shard(reg_n: int, seed: int, rank: int, world: int):
     n = C3_N
     assert B * n <= reg_n
     perm = np.random.default_rng(seed).permutation(reg_n).astype(np.uint32)[: B * n].reshape(B, n)
-    lo, hi = shard_bounds(B, rank, world)
+    lo, hi = shard_bounds_by_work(np.arange(B + 1, dtype=np.int64) * n, rank, world)
     idx2d = perm[lo:hi]
     msgs = b"".join(_msg(b"epoch", seed, j) for j in range(lo, hi))
     return idx2d.reshape(-1), np.arange(hi - lo + 1, dtype=np.uint64) * n, msgs, _agg_sks(idx2d), (lo, hi)

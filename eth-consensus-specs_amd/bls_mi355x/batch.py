@@ -427,6 +427,7 @@ class ResidentFavBatch:
             if u + depth < len(units):
                 k2, ch2 = units[u + depth]
                 self.submit((u + depth) % FAV_JOBS, seeds[k2], ch2)
+        self.ctx.check(self.ctx.lib.bls_sync(self.ctx.h))  # a failing job's bisection writes its verdicts async
         return oks
 
     def verdicts(self) -> np.ndarray:

@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
+
 from . import _native
 
 PARTIAL_BYTES = 576
@@ -51,3 +53,37 @@ def shard_bounds(total: int, rank: int, world: int) -> tuple[int, int]:
     base, extra = divmod(total, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+# per-aggregate work that does not scale with its committee, in pubkey additions: the SURVEY.md §8(d) model
+# prices FAV(n) at 11 (n - 1) + 14,789 FME, i.e. ~1,344 additions' worth per aggregate beside its n - 1 additions
+ITEM_WORK_KEYS = 14789 // 11
+
+
+def shard_bounds_by_work(offsets, rank: int, world: int, per_item: int = ITEM_WORK_KEYS) -> tuple[int, int]:
+    """Contiguous [lo, hi) block of aggregates owned by `rank`, balanced by work ("contiguous
+    blocks of aggregates, balanced by total pubkey count"): aggregate i costs n_i + per_item, n_i =
+    offsets[i + 1] - offsets[i] (per_item = 0: pure pubkey count).  Rank r's block starts at the aggregate whose
+    cumulative work is nearest r / world of the total, so every rank's share is within one aggregate's work of
+    total / world; uniform committees give shard_bounds' blocks.  Every rank computes the same cut points from
+    the same offsets (no exchange)."""
+    offs = np.asarray(offsets, dtype=np.int64)
+    B = int(offs.size) - 1
+    if B <= 0:
+        return 0, 0
+    cum = offs - offs[0] + per_item * np.arange(B + 1, dtype=np.int64)  # work before aggregate i
+    total = int(cum[-1])
+
+    def cut(r: int) -> int:
+        if r <= 0:
+            return 0
+        if r >= world:
+            return B
+        t = total * r / world
+        i = int(np.searchsorted(cum, t))  # first boundary with work >= t
+        if i > 0 and (i > B or t - cum[i - 1] <= cum[i] - t):
+            i -= 1
+        return min(max(i, 0), B)
+
+    lo, hi = cut(rank), cut(rank + 1)
+    return lo, max(lo, hi)

@@ -34,21 +34,28 @@ whether it fires at the call or at the end of the block.  But some sites
 is_valid_deposit_signature(...)`` (specs/electra/beacon-chain.md:932,1555):
 an invalid proof of possession there skips the deposit and the block stays
 valid (test_process_deposit.py:255-287).  Returning a recorded True there
-would apply the deposit and then reject the block.  So ``try_defer`` looks at
-the caller's bytecode: the call is deferred only if its value flows, through
-``return`` statements only, into an ``assert`` (``POP_JUMP_IF_TRUE`` followed
-by ``LOAD_ASSERTION_ERROR``), and every caller on the way calls exactly the
-function below it (no C-level caller such as ``map`` or ``any`` in between);
-any other use -- ``if``, ``not``, a comparison, an assignment -- runs the call
-at once and returns its real verdict.  The bytecode reading is for Python
-3.10 (this image's interpreter); on other versions every call runs at once.
+would apply the deposit and then reject the block.  So ``try_defer`` reads the
+caller's *source* (``ast`` over ``linecache``, the same lines tracebacks show:
+the generated pyspec modules are ordinary files): the call is deferred only if
+every call of that function on the caller's current line is the test of an
+``assert`` statement, or the value of a ``return`` statement whose function's
+own call site (one frame up) satisfies the same rule, and so on.  Any other use
+-- ``if``, ``not``, a comparison, an argument, an assignment, a conditional
+expression, a lambda or a C-level caller such as ``map`` or ``any`` in between
+(it leaves no frame, so the next frame's line calls ``any``, not the function
+below) -- runs the call at once and returns its real verdict, as does a caller
+whose source cannot be read.  Nothing depends on the interpreter's bytecode,
+so every CPython the reference supports (``requires-python = ">=3.10, <3.14"``,
+pyproject.toml:10) batches the same calls; on 3.11+ the instruction's source
+position narrows the match to the exact call expression.
 """
 from __future__ import annotations
 
+import ast
 import contextlib
-import dis
+import itertools
+import linecache
 import sys
-import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -57,124 +64,90 @@ from . import batch as _batch
 
 FAV, VERIFY, AV = "fav", "verify", "av"
 
-_CODE_INDEX: dict = {}  # code object -> (instructions, {offset: position})
-
-# Python 3.10 stack effects (pops, pushes) of the opcodes that build call expressions; a span with any other
-# opcode is not simulated (the call then runs at once -- never a wrong verdict, only no batching)
-_LOADS = {"LOAD_GLOBAL", "LOAD_NAME", "LOAD_FAST", "LOAD_DEREF", "LOAD_CONST", "LOAD_CLOSURE", "LOAD_CLASSDEREF"}
-_FIXED = {"LOAD_ATTR": (1, 1), "LOAD_METHOD": (1, 2), "BINARY_SUBSCR": (2, 1), "COMPARE_OP": (2, 1),
-          "IS_OP": (2, 1), "CONTAINS_OP": (2, 1), "UNARY_NOT": (1, 1), "UNARY_NEGATIVE": (1, 1),
-          "UNARY_INVERT": (1, 1), "UNARY_POSITIVE": (1, 1), "LIST_TO_TUPLE": (1, 1), "GET_ITER": (1, 1),
-          "DUP_TOP": (1, 2), "NOP": (0, 0), "DICT_MERGE": (1, 0), "DICT_UPDATE": (1, 0), "LIST_EXTEND": (1, 0),
-          "SET_UPDATE": (1, 0), "LIST_APPEND": (1, 0), "SET_ADD": (1, 0), "MAP_ADD": (2, 0)}
+_AST_CACHE: dict = {}  # filename -> (linecache lines object, {callee name: [(Call node, parent node)]})
 
 
-def _index(code):
-    ent = _CODE_INDEX.get(code)
-    if ent is None:
-        ins = list(dis.get_instructions(code))
-        ent = (ins, {x.offset: i for i, x in enumerate(ins)})
-        _CODE_INDEX[code] = ent
-    return ent
+def _call_index(frame):
+    """Call nodes of the frame's source file by callee name (``bls.Verify(...)`` -> "Verify", ``fn(...)`` ->
+    "fn"), each with its parent node; None when the source is not available."""
+    fn = frame.f_code.co_filename
+    lines = linecache.getlines(fn, frame.f_globals)
+    if not lines:
+        return None
+    ent = _AST_CACHE.get(fn)
+    if ent is not None and ent[0] is lines:
+        return ent[1]
+    try:
+        tree = ast.parse("".join(lines), fn)
+    except (SyntaxError, ValueError):
+        return None
+    index: dict = {}
+    for parent in ast.walk(tree):
+        for child in ast.iter_child_nodes(parent):
+            if isinstance(child, ast.Call):
+                f = child.func
+                name = f.id if isinstance(f, ast.Name) else (f.attr if isinstance(f, ast.Attribute) else None)
+                if name:
+                    index.setdefault(name, []).append((child, parent))
+    _AST_CACHE[fn] = (lines, index)
+    return index
 
 
-def _next_ops(code, lasti: int, k: int = 2) -> list[str]:
-    """Opnames of the k instructions after the one at byte offset `lasti` ([] if unknown).  TO_BOOL (3.13+,
-    before a conditional jump) is skipped: reserved for a future bytecode port, since callee_name only reads
-    3.10 bytecode and nothing is deferred on other versions (SignatureSets.version_fallback counts those)."""
-    ins, pos = _index(code)
-    i = pos.get(lasti)
-    if i is None:
+def _position(frame):
+    """(lineno, end_lineno, col, end_col) of the frame's current instruction (CPython 3.11+), else None."""
+    positions = getattr(frame.f_code, "co_positions", None)
+    if positions is None or frame.f_lasti < 0:
+        return None
+    try:
+        return next(itertools.islice(positions(), frame.f_lasti // 2, None))
+    except (StopIteration, ValueError):
+        return None
+
+
+def call_sites(frame, callee: str) -> list:
+    """The calls of `callee` in the frame's source that its current instruction can be: every call of that name
+    whose lines span the frame's line -- on 3.11+ only the one whose span is the instruction's, when exactly one
+    is."""
+    index = _call_index(frame)
+    if index is None:
         return []
-    return [x.opname for x in ins[i + 1:] if x.opname != "TO_BOOL"][:k]
+    ln = frame.f_lineno
+    cands = [(c, p) for c, p in index.get(callee, ()) if c.lineno <= ln <= (c.end_lineno or c.lineno)]
+    pos = _position(frame)
+    if pos is not None and len(cands) > 1:
+        exact = [(c, p) for c, p in cands if (c.lineno, c.end_lineno, c.col_offset, c.end_col_offset) == tuple(pos)]
+        if len(exact) == 1:
+            return exact
+    return cands
 
 
-def _pops_pushes(x):
-    op, a = x.opname, x.arg
-    if op in _LOADS:
-        return 0, 1
-    if op in _FIXED:
-        return _FIXED[op]
-    if op.startswith("BINARY_") or op.startswith("INPLACE_"):
-        return 2, 1
-    if op in ("BUILD_TUPLE", "BUILD_LIST", "BUILD_SET", "BUILD_STRING", "BUILD_SLICE"):
-        return a, 1
-    if op == "BUILD_MAP":
-        return 2 * a, 1
-    if op == "BUILD_CONST_KEY_MAP":
-        return a + 1, 1
-    if op == "CALL_FUNCTION":
-        return a + 1, 1
-    if op in ("CALL_FUNCTION_KW", "CALL_METHOD"):
-        return a + 2, 1
-    if op == "CALL_FUNCTION_EX":
-        return 2 + (a & 1), 1
-    if op == "FORMAT_VALUE":
-        return 1 + (1 if (a & 4) else 0), 1
-    return None
-
-
-def callee_name(code, lasti: int) -> str | None:
-    """Name of the callable invoked by the call instruction at byte offset `lasti` (Python 3.10 bytecode), or
-    None when it cannot be determined: the straight-line span back to the nearest jump target is simulated
-    with a symbolic stack whose entries remember the name they were loaded under (``bls.Verify`` ->
-    "Verify", ``is_valid_indexed_attestation`` -> itself, ``any`` -> "any")."""
-    if sys.version_info[:2] != (3, 10):
-        return None
-    ins, pos = _index(code)
-    i = pos.get(lasti)
-    if i is None or not ins[i].opname.startswith("CALL_"):
-        return None
-    lo = i
-    while lo > 0 and not ins[lo].is_jump_target:
-        lo -= 1
-    stack: list = []  # producer name per entry; the entries below the span are unknown (None)
-    for x in ins[lo:i]:
-        if "JUMP" in x.opname or x.opname in ("RETURN_VALUE", "FOR_ITER", "SETUP_FINALLY", "SETUP_WITH"):
-            stack = []  # control flow inside the span: nothing below is known
-            continue
-        pp = _pops_pushes(x)
-        if pp is None:
-            return None
-        pops, pushes = pp
-        if x.opname == "DUP_TOP":
-            top = stack[-1] if stack else None
-            stack.append(top)
-            continue
-        for _ in range(pops):
-            if stack:
-                stack.pop()
-        name = x.argval if x.opname in _LOADS or x.opname in ("LOAD_ATTR", "LOAD_METHOD") else None
-        if x.opname == "LOAD_METHOD":
-            stack.extend([name, None])  # (method, self) / (NULL, callable)
-        else:
-            stack.extend([name if isinstance(name, str) else None] * pushes)
-    pops, _ = _pops_pushes(ins[i])
-    if len(stack) < pops:
-        return None
-    return stack[-pops]
+def _use(call, parent) -> str:
+    if isinstance(parent, ast.Assert) and parent.test is call:
+        return "assert"
+    if isinstance(parent, ast.Return) and parent.value is call:
+        return "return"
+    return "other"
 
 
 def result_is_asserted(frame, callee: str) -> bool:
     """True iff the value that the call to `callee` (the function `frame` is executing a call into) returns
-    reaches an ``assert`` through ``return`` statements only, walking up the callers.  At every level the
-    caller's instruction must be a call of exactly that function: a C-level caller in between (``map``,
-    ``any``, ``sorted`` ...) leaves no Python frame, so ``assert any(map(bls.Verify, ...))`` shows a call of
-    ``any`` there and the verdict is computed at once."""
+    reaches an ``assert`` through ``return`` statements only, walking up the callers.  At every level every
+    call of that function on the caller's current line must be such a use: a C-level caller in between (``map``,
+    ``any``, ``sorted`` ...) leaves no Python frame, so ``assert any(map(bls.Verify, ...))`` shows calls of
+    ``any`` and ``map`` there, not of ``Verify``, and the verdict is computed at once."""
     depth = 0
     while frame is not None and depth < 32:
-        if callee_name(frame.f_code, frame.f_lasti) != callee:
+        sites = call_sites(frame, callee)
+        if not sites:
             return False
-        ops = _next_ops(frame.f_code, frame.f_lasti)
-        if not ops:
+        uses = {_use(c, p) for c, p in sites}
+        if uses == {"assert"}:
+            return True
+        if uses != {"return"}:
             return False
-        if ops[0] == "RETURN_VALUE":
-            callee = frame.f_code.co_name
-            frame = frame.f_back
-            depth += 1
-            continue
-        return (ops[0].startswith("POP_JUMP") and ops[0].endswith("IF_TRUE") and len(ops) > 1
-                and ops[1] == "LOAD_ASSERTION_ERROR")
+        callee = frame.f_code.co_name
+        frame = frame.f_back
+        depth += 1
     return False
 
 
@@ -200,7 +173,6 @@ class SignatureSets:
         self.ctx = ctx
         self.sets: list[_Set] = []
         self.eager = 0  # verify calls inside deferred() that ran at once (result not asserted)
-        self.version_fallback = 0  # of those, calls run at once only because this interpreter is not 3.10
 
     def try_defer(self, kind: str, args) -> bool:
         """Called by the shim's Verify / FastAggregateVerify / AggregateVerify (bls.py ``_defer``): record the
@@ -209,14 +181,6 @@ class SignatureSets:
         caller = shim_fn.f_back  # only_with_bls's wrapper (named like the shim function), calling it as `fn`
         callee = "fn" if caller is not None and caller.f_code.co_name == shim_fn.f_code.co_name else \
             shim_fn.f_code.co_name
-        if sys.version_info[:2] != (3, 10):  # the bytecode walk reads 3.10 only: batching is lost, say so once
-            self.eager += 1
-            self.version_fallback += 1
-            if self.version_fallback == 1:
-                warnings.warn(f"bls_mi355x.sigsets: deferred() batching needs Python 3.10 bytecode; on "
-                              f"{sys.version_info[0]}.{sys.version_info[1]} every verify call runs at once",
-                              RuntimeWarning, stacklevel=4)
-            return False
         if not result_is_asserted(caller, callee):
             self.eager += 1
             return False

@@ -21,9 +21,9 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
+  S_FAV_F, S_FAV_FT, S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
-  S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD,
+  S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD, S_BSIG, S_BRSC, S_BLINES,
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
   S_AV_IO, S_AV_RSC, S_AV_PITEM, S_AV_SIG, S_AV_SOK, S_AV_H, S_AV_ST, S_AV_P, S_AV_Q, S_AV_F, S_AV_FT, S_AV_SEL,
   S_AV_FI, S_AV_RES, S_AV_HCF, S_AV_FLAG, S_AV_ML,
@@ -35,7 +35,7 @@ enum Slot {
   S_PT_IN, S_PT_A, S_PT_OK, S_PT_TMP, S_PT_OUT,
   // per-call Verify / FastAggregateVerify pair points (not S_RP: a FAV batch's r_i apk_i live there between its
   // partial and finish calls, and fav_bisect reads them back)
-  S_PC_P, S_PC_L,
+  S_PC_P,
   NSLOT
 };
 
@@ -58,14 +58,22 @@ struct Job {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_sig = nullptr, ev_msm = nullptr, ev_gather = nullptr;
   hipEvent_t ev_partial = nullptr;  // the batch's 576-byte partial is in h_partial
   hipEvent_t ev_h2c = nullptr, ev_fb = nullptr, ev_fe = nullptr;  // hand-offs to the context-wide aux streams
+  // a bisection has copied what it reads of the batch state that stream2 / stream3 overwrite: the job's next batch
+  // starts its hash and signature branches from here instead of after the whole bisection (fav_prepare)
+  hipEvent_t ev_bis = nullptr;
+  bool bis_pending = false;
   uint8_t* h_partial = nullptr;     // pinned host copy of the partial
   Buf buf[NSLOT];
   // last prepared FAV batch
   size_t fav_B = 0;
   bool fav_ready = false;
   bool partial_pending = false;
-  // last bisection fallback: batched final-exponentiation checks and rounds
+  bool own_check_failed = false;  // the last check of this job was of its own partial alone, and it failed
+  int fav_mg = 1;  // pairs per f of the prepared batch's Miller accumulation
+  // last bisection fallback: final-exponentiation checks and rounds (levels); the checks of a FAV bisection are
+  // counted on the device (bis_dev_checks, read after the job's stream by bls_last_fallback_stats)
   uint64_t bis_checks = 0, bis_rounds = 0;
+  uint32_t* bis_dev_checks = nullptr;
 };
 
 struct bls_ctx {
@@ -75,6 +83,8 @@ struct bls_ctx {
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
   std::string err;
+  G1A* comb = nullptr;  // -G1 comb of the bisection fallback (bls_bisect.hip), built on first use
+  Job* stats_job = &jobs[0];  // the job whose fallback statistics bls_last_fallback_stats reports
   // Context-wide streams for the kernels with large private segments (the h2c
   // fallback, 6,000 B/lane; final-exponentiation checks, 3,296 B/lane): the
   // runtime gives every hardware queue that runs such a kernel a scratch
@@ -251,18 +261,15 @@ void prof_collect(bls_ctx* c) {
 
 // Final-exponentiation check of the product of f[0 .. n) on the context's FE
 // stream, after the current job's stream: 1 / 0.
-int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1, bool percall = false) {
+int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
   int* d_r;
   SCR(S_INT, 4, d_r);
   Job& J = *ctx->j;
   HIPCK(hipEventRecord(J.ev_fe, J.stream));
   HIPCK(hipStreamWaitEvent(ctx->fe_stream, J.ev_fe, 0));
-  // per-call checks on the six-wave k_fe_wide (latency); batch checks on the one-wave k_fe_check, which leaves the
-  // CU to the other jobs (profiles/r04m_fe_ab.txt: 1.92 M vs 1.84 M FAV/s with every check six-wave)
-  if (percall)
-    PROF2(7, ctx->fe_stream, launch_fe_wide(ctx->fe_stream, f, n, d_r));
-  else
-    PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
+  // batch checks on the one-wave k_fe_check, which leaves the CU to the other jobs (profiles/r04m_fe_ab.txt: 1.92 M vs
+  // 1.84 M FAV/s with every check six-wave); the per-call path runs k_fe_wide on its own stream (verify_percall)
+  PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
   int r = 0;
   HIPCK(hipMemcpyAsync(&r, d_r, sizeof r, hipMemcpyDeviceToHost, ctx->fe_stream));
   HIPCK(hipStreamSynchronize(ctx->fe_stream));
@@ -295,8 +302,9 @@ __global__ void k_or_flags(size_t B, const int* force, int* flag) {
 int h2c_fallback(bls_ctx* ctx, hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, int* flag,
                  G2A* H) {
   Job& J = *ctx->j;
-  if (ctx->force_fb && B && B <= ctx->force_fb_n) {  // test hook only
-    hipLaunchKernelGGL(k_or_flags, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, B, ctx->force_fb, flag);
+  if (ctx->force_fb && B) {  // test hook only: the mask's items i < min(B, n)
+    const size_t nf = B < ctx->force_fb_n ? B : ctx->force_fb_n;
+    hipLaunchKernelGGL(k_or_flags, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st, nf, ctx->force_fb, flag);
     LK(hipGetLastError());
   }
   HIPCK(hipEventRecord(J.ev_h2c, st));
@@ -357,6 +365,7 @@ static bool job_init(Job& J, int prio_hi) {
          hipEventCreateWithFlags(&J.ev_h2c, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_fb, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_fe, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_bis, hipEventDisableTiming) == hipSuccess &&
          hipHostMalloc((void**)&J.h_partial, 576, hipHostMallocDefault) == hipSuccess;
 }
 
@@ -366,7 +375,8 @@ static void job_destroy(Job& J) {
     if (s) (void)hipStreamSynchronize(s);
   for (auto& b : J.buf)
     if (b.p) (void)hipFree(b.p);
-  hipEvent_t es[9] = {J.ev_fork, J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial, J.ev_h2c, J.ev_fb, J.ev_fe};
+  hipEvent_t es[10] = {J.ev_fork, J.ev_join, J.ev_sig,  J.ev_msm, J.ev_gather,
+                       J.ev_partial, J.ev_h2c, J.ev_fb, J.ev_fe, J.ev_bis};
   for (hipEvent_t e : es)
     if (e) (void)hipEventDestroy(e);
   if (J.h_partial) (void)hipHostFree(J.h_partial);
@@ -438,16 +448,15 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
 }
 
 // Per-call CoreVerify over n keys (n = 1: Verify, E/utils/bls.py:141-151;
-// n > 1: FastAggregateVerify, :167-177), on the three streams of job 0:
-//   stream2: hash_to_G2(msg) (lane SSWU + wave-program isogeny / cofactor phases)
-//   stream3: signature decode + G2 subgroup check
-//   stream1: KeyValidate of every key (+ their sum)
-// The Miller loop of (-G1, sigma) runs on stream3 right after the signature
-// check, while hash_to_G2 is still running; stream1 then runs only the Miller
-// loop of (apk, H(m)) after the hash, one Fp12 product and one final-
-// exponentiation check.  Every chain that can be spread over a workgroup is
-// (the h2c and pairing phases); only the square roots and subgroup checks run
-// one lane each.
+// n > 1: FastAggregateVerify, :167-177), on the three streams of job 0, in
+// wavefront-cooperative arithmetic:
+//   stream2: hash_to_G2(msg) on one wave (k_h2c_wide)
+//   stream3: signature decode + G2 subgroup check (k_sig_validate_wide)
+//   stream1: KeyValidate of every key (+ their sum), then -- after both
+//            branches -- the Miller loops of (apk, H) and (-G1, sigma) fused on
+//            ONE k_miller_wide workgroup, the six-wave final exponentiation
+//            (k_fe_wide) on the same stream, and both verdict words (FE, live)
+//            back in one pinned copy.
 static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
                           const uint8_t* sig96) {
   Job& J = *ctx->j;
@@ -457,7 +466,6 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   G2A* Q;
   int *ok, *d_r;
   G1J *tmp, *apk;
-  Fd* hf;
   int* flag;
   Fp12* f;
   uint64_t* d_offs;
@@ -472,7 +480,6 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_G2A, 2, Q);
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
-  SCR(S_AV_HCF, h2c_scratch_fd(1), hf);
   SCR(S_AV_FLAG, 1, flag);
   SCR(S_F, 3, f);  // f(apk, H) | f(-G1, sigma) | their product
   SCR(S_INT, 4, d_r);
@@ -498,7 +505,6 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   // one wave of wavefront-cooperative arithmetic for the one message (bls_wide.h); 32-byte messages (every
   // signing root) take the register-resident expand_message_xmd
   const uint64_t* h_offs = msg_len == 32 ? nullptr : d_offs;
-  (void)hf;
   LK(launch_h2c_wide(st2, 1, d_msg, h_offs, Q, flag));
   CK(h2c_fallback(ctx, st2, 1, d_msg, h_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
@@ -1028,20 +1034,29 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_MLINES, miller_lines_u32(B), mlines);
   SCR(S_SAFF, 1, saff);
   SCR(S_MSTAT, B, dstat);
-  SCR(S_F, B + 2, f);
-  SCR(S_F_T, (B + 1) / 8 + 16, ft);
+  SCR(S_FAV_F, B + 2, f);  // per-item (or per-group) f, kept for the bisection: not S_F, which per-call checks use
+  SCR(S_FAV_FT, (B + 1) / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   SCR(S_SEED, 32, d_seed);
-  CK(h2d(ctx, d_seed, seed32, 32));
   hipStream_t st = ctx->j->stream, st2 = ctx->j->stream2, st3 = ctx->j->stream3;
+  // the branches fork from stream1's tail -- or, after a bisection still running there, from the point where it
+  // has copied everything it reads of the state stream2 / stream3 write (fav_bisect); the seed goes on stream3,
+  // its reader, so the fork need not follow stream1
+  HIPCK(hipMemcpyAsync(d_seed, seed32, 32, hipMemcpyHostToDevice, st3));
   // Three branches:
   //   stream1: registry gather (affine apk) -> subgroup / r_i apk_i chains -> Miller loops
   //   stream2: hash_to_G2 of every message
   //   stream3: signature decompression + RLC scalars -> MSM S = sum r_i sigma_i
   //            -> Miller loop of (-G1, S) -> f[B + 1]
-  HIPCK(hipEventRecord(ctx->j->ev_fork, st));
-  HIPCK(hipStreamWaitEvent(st2, ctx->j->ev_fork, 0));
-  HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_fork, 0));
+  hipEvent_t fork = ctx->j->ev_fork;
+  if (ctx->j->bis_pending) {
+    fork = ctx->j->ev_bis;
+    ctx->j->bis_pending = false;
+  } else {
+    HIPCK(hipEventRecord(fork, st));
+  }
+  HIPCK(hipStreamWaitEvent(st2, fork, 0));
+  HIPCK(hipStreamWaitEvent(st3, fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, hcf, H, flag));
   CK(h2c_fallback(ctx, st2, B, d_msgs, nullptr, flag, H));
   PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
@@ -1075,6 +1090,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   // launch under-fills the chip and the chain latency is what counts, so one pair per f (a step is a squaring
   // and ONE line: ~37 % shorter chains for ~24 % more products)
   const int mg = B >= ACC_SHARED_MIN ? 2 : 1;
+  ctx->j->fav_mg = mg;
   PROF(5, launch_miller_acc4(st, rP, H, status, B, mlines, f, mg));
   PROF(6, launch_fp12_prod_vm(st, f, (B + mg - 1) / mg, ft, f + B));
   HIPCK(hipStreamWaitEvent(st, ctx->j->ev_msm, 0));
@@ -1086,78 +1102,100 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
 }
 
 // Bisection fallback ("a failing batch falls back to
-// per-signature bisection").  Per-item Miller values f_i of the pairs
-// (r_i apk_i, H_i), (-r_i G1, sigma_i) form the leaves of a 16-ary product
-// tree; each round final-exponentiates, in one batched launch, the children of
-// the nodes that failed the round before.  A leaf that fails is an invalid
+// per-signature bisection"), on the job's own stream with no host round trip.
+// The leaves are the items' Miller values from the batch's own kernels:
+//   f_H,i   = ML(r_i apk_i, H_i): the batch's per-item f (one pair per f below
+//             ACC_SHARED_MIN items) or k_miller_acc4q<1> over the batch's line
+//             records again (shared-f batches);
+//   f_sig,i = ML(-r_i G1, sigma_i): -r_i G1 from a fixed-base comb (8 mixed
+//             additions), sigma_i's line records by k_miller_lines2 (written over
+//             the H records, which are no longer needed), f by k_miller_acc4q<1>;
+// leaf_i = f_H,i f_sig,i, and a 16-ary product tree above the leaves.  A node's
+// check is FE(node) == 1: the product of e(r_i apk_i, H_i) e(-r_i G1, sigma_i)
+// over its items, the random linear combination of their checks.  The first
+// checked level is the lowest with at most 64 nodes (all of them checked; the
+// root first when the caller does not know it fails); every level below is one
+// launch of k_fe_check_gated that checks exactly the nodes whose parent failed,
+// reading the parent's result on the device.  A leaf that fails is an invalid
 // item; every item under a passing node keeps its per-item status.  With k bad
-// items among B this costs about 16 k log16(B / k) checks in log16(B) rounds
-// instead of B checks.  root_bad: the caller already knows the product fails.
+// items among B this is ~64 + 16 k (log16(B) - 2) checks.  Items with status 0
+// (rejected before the pairing) have leaf 1 and keep verdict 0.  root_bad: the
+// caller already knows the product fails.
 static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
-  const size_t B = ctx->j->fav_B;
-  const int* status = (const int*)ctx->j->buf[S_STATUS].p;
-  const uint64_t* rsc = (const uint64_t*)ctx->j->buf[S_RSC].p;
-  const G1A* rP = (const G1A*)ctx->j->buf[S_RP].p;
-  const G2A* H = (const G2A*)ctx->j->buf[S_H].p;
-  const G2A* sig = (const G2A*)ctx->j->buf[S_SIG].p;
+  Job& J = *ctx->j;
+  const size_t B = J.fav_B;
+  const int* status = (const int*)J.buf[S_STATUS].p;
+  const uint64_t* rsc0 = (const uint64_t*)J.buf[S_RSC].p;
+  const G1A* rP = (const G1A*)J.buf[S_RP].p;
+  const G2A* H = (const G2A*)J.buf[S_H].p;
+  const G2A* sig0 = (const G2A*)J.buf[S_SIG].p;
+  Fp12* fb = (Fp12*)J.buf[S_FAV_F].p;
+  const uint32_t* mlines = (const uint32_t*)J.buf[S_MLINES].p;
   std::vector<size_t> off{0}, cnt{B};
   while (cnt.back() > 1) {
     off.push_back(off.back() + cnt.back());
     cnt.push_back((cnt.back() + 15) / 16);
   }
-  const size_t total = off.back() + cnt.back();
-  G1A* P2;
-  G2A* Q2;
-  int *st2, *d_res;
-  Fp12* tree;
-  uint32_t* d_sel;
-  uint8_t* d_bad;
-  SCR(S_BP, 2 * B, P2);
-  SCR(S_BQ, 2 * B, Q2);
-  SCR(S_BS, 2 * B, st2);
+  const int R = (int)cnt.size() - 1;
+  int T = 0;  // first checked level below the root: the lowest with at most 64 nodes
+  while (T < R && cnt[T] > 64) T++;
+  const int top = root_bad ? T : R;  // highest level the tree must be built to
+  const size_t total = off[top] + cnt[top];
+  G1A* Ps;
+  G1P* Pj;
+  Fp12 *fS, *fH, *tree;
+  int* res;
+  uint32_t *nchk, *slines;
+  G2A* sig;
+  uint64_t* rsc;
+  SCR(S_BP, B, Ps);
+  SCR(S_BQ, B, Pj);
+  SCR(S_BS, B, fS);
   SCR(S_BT, total, tree);
-  SCR(S_BSEL, B + 16, d_sel);
-  SCR(S_BRES, B + 16, d_res);
-  SCR(S_BBAD, B, d_bad);
-  hipStream_t st = ctx->j->stream;
-  LK(launch_bisect_pairs(st, B, rsc, status, rP, H, sig, P2, Q2, st2));
-  LK(launch_miller2(st, P2, Q2, st2, 2 * B, tree));
-  for (size_t L = 0; L + 1 < cnt.size(); L++)
-    LK(launch_fp12_chunk_prod(st, tree + off[L], cnt[L], 16, tree + off[L + 1]));
-  std::vector<uint8_t> bad(B, 0);
-  std::vector<uint32_t> cand, sel;
-  std::vector<int> res;
-  int L = (int)cnt.size() - 1;
-  cand.push_back(0);
-  ctx->j->bis_checks = ctx->j->bis_rounds = 0;
-  auto children = [&](int lvl, uint32_t node, std::vector<uint32_t>& next) {
-    for (size_t c = (size_t)node * 16; c < (size_t)node * 16 + 16 && c < cnt[lvl - 1]; c++) next.push_back((uint32_t)c);
-  };
-  if (root_bad && L > 0) {  // skip re-checking the root
-    std::vector<uint32_t> next;
-    children(L, 0, next);
-    cand.swap(next);
-    L--;
+  SCR(S_BRES, total, res);
+  SCR(S_BBAD, 1, nchk);
+  SCR(S_BSIG, B, sig);
+  SCR(S_BRSC, B, rsc);
+  SCR(S_BLINES, miller_lines_u32(B), slines);
+  if (J.fav_mg > 1) SCR(S_BSEL, B, fH);
+  else fH = fb;
+  hipStream_t st = J.stream;
+  if (!ctx->comb) {  // the -G1 comb, once per context
+    HIPCK(hipMalloc(&ctx->comb, neg_g1_comb_entries() * sizeof(G1A)));
+    LK(launch_neg_g1_comb_table(st, ctx->comb));
   }
-  for (; L >= 0 && !cand.empty(); L--) {
-    const size_t n = cand.size();
-    sel.resize(n);
-    for (size_t k = 0; k < n; k++) sel[k] = (uint32_t)(off[L] + cand[k]);
-    res.resize(n);
-    CK(run_final_checks_sel(ctx, tree, sel.data(), n, d_sel, d_res, res.data()));
-    ctx->j->bis_checks += n;
-    ctx->j->bis_rounds += 1;
-    std::vector<uint32_t> next;
-    for (size_t k = 0; k < n; k++) {
-      if (res[k]) continue;
-      if (L == 0) bad[cand[k]] = 1;
-      else children(L, cand[k], next);
-    }
-    cand.swap(next);
+  // first everything read of the state that the job's next batch writes from stream2 / stream3 (H and the line
+  // records, sigma_i, r_i); that batch forks from ev_bis (fav_prepare) while the rest runs here
+  if (J.fav_mg > 1) LK(launch_miller_acc4(st, rP, H, status, B, mlines, fH, 1));
+  HIPCK(hipMemcpyAsync(sig, sig0, B * sizeof(G2A), hipMemcpyDeviceToDevice, st));
+  HIPCK(hipMemcpyAsync(rsc, rsc0, B * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+  HIPCK(hipEventRecord(J.ev_bis, st));
+  J.bis_pending = true;
+  LK(launch_neg_rg1(st, B, status, rsc, ctx->comb, Pj, Ps));
+  LK(launch_miller_lines(st, sig, B, slines));
+  LK(launch_miller_acc4(st, Ps, sig, status, B, slines, fS, 1));
+  LK(launch_fp12_chunk_prod2(st, fH, fS, B, 1, tree));
+  for (int L = 0; L < top; L++) LK(launch_fp12_chunk_prod(st, tree + off[L], cnt[L], 16, tree + off[L + 1]));
+  HIPCK(hipMemsetAsync(nchk, 0, sizeof(uint32_t), st));
+  uint64_t rounds = 0;
+  const int* parent = nullptr;
+  uint32_t pdiv = 1;
+  if (!root_bad && T < R) {  // the root first; level T then runs only if it failed
+    LK(launch_fe_wide_gated(st, tree + off[R], 1, nullptr, 1, res + off[R], nchk));
+    parent = res + off[R];
+    pdiv = (uint32_t)cnt[T];
+    rounds++;
   }
-  CK(h2d(ctx, d_bad, bad.data(), B));
-  LK(launch_verdicts(st, status, d_bad, B, d_out));
-  HIPCK(hipStreamSynchronize(st));  // `bad` is pageable host memory
+  for (int L = T; L >= 0; L--) {
+    LK(launch_fe_wide_gated(st, tree + off[L], cnt[L], parent, pdiv, res + off[L], nchk));
+    parent = res + off[L];
+    pdiv = 16;
+    rounds++;
+  }
+  LK(launch_verdicts_res(st, status, res, B, d_out));
+  J.bis_rounds = rounds;
+  J.bis_dev_checks = nchk;  // read (after the stream) by bls_last_fallback_stats
+  ctx->stats_job = &J;
   return 0;
 }
 
@@ -1170,6 +1208,8 @@ static int fav_finish(bls_ctx* ctx, int batch_ok, bool root_bad, uint8_t* d_out)
   int* status = (int*)ctx->j->buf[S_STATUS].p;
   if (batch_ok) {
     ctx->j->bis_checks = ctx->j->bis_rounds = 0;
+    ctx->j->bis_dev_checks = nullptr;
+    ctx->stats_job = ctx->j;
     PROF(8, launch_status_to_u8(ctx->j->stream, status, B, d_out));
     return 0;
   }
@@ -1277,6 +1317,8 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
     if (msg_offs[total] && !msgs) return BLS_E_ARG;
   }
   ctx->j->bis_checks = ctx->j->bis_rounds = 0;
+  ctx->j->bis_dev_checks = nullptr;
+  ctx->stats_job = ctx->j;
   hipStream_t st = ctx->j->stream;
   const size_t npair = total + B;
   // inputs
@@ -1671,8 +1713,16 @@ int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s9
 
 int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds) {
   API_ENTER(ctx);
-  if (fe_checks) *fe_checks = ctx->j->bis_checks;
-  if (rounds) *rounds = ctx->j->bis_rounds;
+  Job& J = *ctx->stats_job;
+  if (J.bis_dev_checks) {
+    uint32_t n = 0;
+    HIPCK(hipMemcpyAsync(&n, J.bis_dev_checks, sizeof n, hipMemcpyDeviceToHost, J.stream));
+    HIPCK(hipStreamSynchronize(J.stream));
+    J.bis_checks = n;
+    J.bis_dev_checks = nullptr;
+  }
+  if (fe_checks) *fe_checks = J.bis_checks;
+  if (rounds) *rounds = J.bis_rounds;
   return 0;
 }
 
@@ -1700,15 +1750,22 @@ int bls_h2d(bls_ctx* ctx, void* dst, const void* src, size_t bytes) {
   return 0;
 }
 
+// every job stream of the context (a job's bisection fallback writes its verdicts asynchronously)
+static int sync_jobs(bls_ctx* ctx) {
+  for (int k = 0; k < ctx->njobs; k++) HIPCK(hipStreamSynchronize(ctx->jobs[k].stream));
+  return 0;
+}
+
 int bls_d2h(bls_ctx* ctx, void* dst, const void* src, size_t bytes) {
   API_ENTER(ctx);
+  CK(sync_jobs(ctx));
   CK(d2h(ctx, dst, src, bytes));
   return 0;
 }
 
 int bls_sync(bls_ctx* ctx) {
   API_ENTER(ctx);
-  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  CK(sync_jobs(ctx));
   return 0;
 }
 
@@ -1725,6 +1782,7 @@ static int job_submit(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_off
   HIPCK(hipMemcpyAsync(J.h_partial, d_b, 576, hipMemcpyDeviceToHost, J.stream));
   HIPCK(hipEventRecord(J.ev_partial, J.stream));
   J.partial_pending = true;
+  J.own_check_failed = false;
   return 1;
 }
 
@@ -1749,13 +1807,18 @@ static int job_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
   SCR(S_FCHK, n, f);
   CK(h2d(ctx, d_b, partials576, 576 * n));
   PROF(9, launch_fp12_from_bytes(ctx->j->stream, d_b, n, f));
-  return run_final_check(ctx, f, (int)n);  // the n partials are multiplied inside the FE kernel
+  const int r = run_final_check(ctx, f, (int)n);  // the n partials are multiplied inside the FE kernel
+  // one partial equal to this job's own: a failure localises to this job (its bisection skips the root check)
+  ctx->j->own_check_failed = r == 0 && n == 1 && ctx->j->h_partial && !memcmp(partials576, ctx->j->h_partial, 576);
+  return r;
 }
 
+// Verdicts are written on the job's stream: a failing batch's bisection runs there without a host round trip, so
+// the caller can check the next job meanwhile (bls_sync / bls_d2h wait for every job stream).
 static int job_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   if (!d_out) return BLS_E_ARG;
-  CK(fav_finish(ctx, batch_ok, false, d_out));
-  HIPCK(hipStreamSynchronize(ctx->j->stream));
+  CK(fav_finish(ctx, batch_ok, ctx->j->own_check_failed, d_out));
+  ctx->j->own_check_failed = false;
   return 1;
 }
 
@@ -1891,7 +1954,9 @@ static int job_check_comm(bls_ctx* ctx) {
   if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllGather");
   J.partial_pending = false;  // consumed on the device (the pinned host copy is not waited for)
   PROF(9, launch_fp12_from_bytes(J.stream, d_all, W, f));
-  return run_final_check(ctx, f, W);
+  const int ok = run_final_check(ctx, f, W);
+  J.own_check_failed = ok == 0 && W == 1;
+  return ok;
 }
 
 int bls_fav_job_check_comm(bls_ctx* ctx, int job) {

@@ -396,6 +396,12 @@ hipError_t launch_sig_decode(hipStream_t st, size_t B, const uint8_t* msgs32, co
   return hipGetLastError();
 }
 
+hipError_t launch_g1_affine(hipStream_t st, size_t B, const int* status, const G1P* Pj, G1A* out) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_g1_affine_b, dim3(nblk(B, 64 * AFF_K)), dim3(64), 0, st, B, status, Pj, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status, const int* dstat,
                          const G1P* apk_aff, const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP) {
   if (!B) return hipSuccess;

@@ -2,7 +2,7 @@
 // one 64-lane wave, lane-parallel (bls_fe.h: phase executor, tables from
 // tools/gen_fe.py, schedule).  Replaces the wave-program k_final_check_vm on
 // every batch check, bisection round, per-call verification and RCCL
-// exchange (launch_final_check_wave / launch_final_check_sel).
+// exchange (launch_final_check_wave / launch_final_check_sel / launch_final_check_gated).
 //
 // The descriptors of the two operations that make up the hard part -- the
 // cyclotomic squaring (315 calls) and the Fp12 product (~40) -- are loaded
@@ -55,19 +55,12 @@ struct FeDev : FeOps<FeDev> {
 
 }  // namespace
 
-// Product of fin[0 .. n), final exponentiation, *out = (result == 1).  With sel != nullptr, workgroup b checks
-// fin[sel[b]] alone and writes out[b] (the batched checks of a bisection round).
-__global__ void __launch_bounds__(64) k_fe_check(const Fp12* fin, int n, const uint32_t* sel, int* out) {
-  __shared__ FeSlot s[FE_NSLOT];
-  __shared__ int bad;
+// Product of fin[0 .. n), final exponentiation, *out = (result == 1), on the calling 64-lane workgroup.
+__device__ __forceinline__ void fe_check_body(FeSlot* s, int* bad, const Fp12* fin, int n, int* out) {
   const int lane = threadIdx.x;
-  if (sel) {
-    fin += sel[blockIdx.x];
-    out += blockIdx.x;
-  }
   fe_load_consts(s, lane, 64);
   if (lane == 0) {
-    bad = 0;
+    *bad = 0;
     fe_st(s, FE_ABS_BASE + FE_CS, fq_zero());
   }
   FeDev ex;
@@ -82,10 +75,38 @@ __global__ void __launch_bounds__(64) k_fe_check(const Fp12* fin, int n, const u
   fe_schedule(ex);
   if (lane < 12) {
     const Fp v = fq_pack(fe_ld(s, 12 + lane));
-    if (!(lane == 0 ? fp_is_one(v) : fp_is_zero(v))) atomicOr(&bad, 1);
+    if (!(lane == 0 ? fp_is_one(v) : fp_is_zero(v))) atomicOr(bad, 1);
   }
   __syncthreads();
-  if (lane == 0) *out = bad ? 0 : 1;
+  if (lane == 0) *out = *bad ? 0 : 1;
+}
+
+// With sel != nullptr, workgroup b checks fin[sel[b]] alone and writes out[b] (AggregateVerify per-item checks).
+__global__ void __launch_bounds__(64) k_fe_check(const Fp12* fin, int n, const uint32_t* sel, int* out) {
+  __shared__ FeSlot s[FE_NSLOT];
+  __shared__ int bad;
+  if (sel) {
+    fin += sel[blockIdx.x];
+    out += blockIdx.x;
+  }
+  fe_check_body(s, &bad, fin, n, out);
+}
+
+// One level of the bisection tree (bls_capi.hip fav_bisect): workgroup b checks node[b] only when its parent
+// failed -- parent == nullptr (the level's nodes are all checked) or parent[b / pdiv] == 0 -- and otherwise
+// inherits the parent's pass (res[b] = 1) without a check.  The gate is read on the device, so the rounds of a
+// bisection are launched back to back with no host round trip; *nchecks counts the checks that ran.
+__global__ void __launch_bounds__(64) k_fe_check_gated(const Fp12* node, const int* parent, uint32_t pdiv, int* res,
+                                                       uint32_t* nchecks) {
+  __shared__ FeSlot s[FE_NSLOT];
+  __shared__ int bad;
+  const uint32_t b = blockIdx.x;
+  if (parent && parent[b / pdiv]) {  // uniform over the workgroup: it leaves before any barrier
+    if (threadIdx.x == 0) res[b] = 1;
+    return;
+  }
+  if (threadIdx.x == 0) atomicAdd(nchecks, 1u);
+  fe_check_body(s, &bad, node + b, 1, res + b);
 }
 
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out) {
@@ -96,6 +117,13 @@ hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* ou
 hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out) {
   if (!nsel) return hipSuccess;
   hipLaunchKernelGGL(k_fe_check, dim3((unsigned)nsel), dim3(64), 0, st, f, 1, sel, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_final_check_gated(hipStream_t st, const Fp12* node, size_t n, const int* parent, uint32_t pdiv,
+                                    int* res, uint32_t* nchecks) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fe_check_gated, dim3((unsigned)n), dim3(64), 0, st, node, parent, pdiv, res, nchecks);
   return hipGetLastError();
 }
 

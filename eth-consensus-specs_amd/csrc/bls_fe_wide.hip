@@ -157,7 +157,21 @@ struct FeWide {
   }
 };
 
-__global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const uint32_t* sel, int* out, uint64_t* ts) {
+// sel: workgroup b checks fin[sel[b]] into out[b].  nchecks != nullptr (the bisection tree's levels, bls_capi.hip
+// fav_bisect): workgroup b checks fin[b] into out[b] when parent is null or parent[b / pdiv] == 0 (and counts it in
+// *nchecks), else out[b] = 1 without a check.
+__global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const uint32_t* sel, int* out, uint64_t* ts,
+                                                 const int* parent, uint32_t pdiv, uint32_t* nchecks) {
+  if (nchecks) {
+    const uint32_t b = blockIdx.x;
+    fin += b;
+    out += b;
+    if (parent && parent[b / pdiv]) {  // uniform over the workgroup: it leaves before any barrier
+      if (threadIdx.x == 0) *out = 1;
+      return;
+    }
+    if (threadIdx.x == 0) atomicAdd(nchecks, 1u);
+  }
   int nts = 0;
   auto stamp = [&]() {
     if (ts && threadIdx.x == 0) ts[nts] = wall_clock64();
@@ -226,7 +240,16 @@ __global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const u
 }
 
 hipError_t launch_fe_wide(hipStream_t st, const Fp12* f, int n, int* out, uint64_t* ts) {
-  hipLaunchKernelGGL(k_fe_wide, dim3(1), dim3(384), 0, st, f, n, (const uint32_t*)nullptr, out, ts);
+  hipLaunchKernelGGL(k_fe_wide, dim3(1), dim3(384), 0, st, f, n, (const uint32_t*)nullptr, out, ts, (const int*)nullptr,
+                     1u, (uint32_t*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_fe_wide_gated(hipStream_t st, const Fp12* node, size_t n, const int* parent, uint32_t pdiv, int* res,
+                                uint32_t* nchecks) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fe_wide, dim3((unsigned)n), dim3(384), 0, st, node, 1, (const uint32_t*)nullptr, res,
+                     (uint64_t*)nullptr, parent, pdiv, nchecks);
   return hipGetLastError();
 }
 

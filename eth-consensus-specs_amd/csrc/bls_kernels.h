@@ -18,7 +18,6 @@ hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, ui
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const RegKey* reg, uint32_t reg_n, G1P* apk, int* status);
 // registry entries from k_key_validate output (+ the host validity mask)
 hipError_t launch_reg_pack(hipStream_t st, const G1A* a, const int* ok, size_t n, RegKey* reg, uint8_t* valid);
-hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP, const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2);
 hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok, const G2A* sig, const uint64_t* rsc, int* status, G1A* P2, G2A* Q2);
 hipError_t launch_av_pairs(hipStream_t st, size_t total, const uint32_t* pair_item, const int* status, const uint64_t* rsc, const G1A* pk, const G2A* H, G1A* P2, G2A* Q2);
 // out[b] = product of in[io[b] + b .. io[b + 1] + b] (the AggregateVerify batch's per-item segments)
@@ -71,8 +70,25 @@ hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t*
 // four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values
 hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                               Fp12* f, int G);
-hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
+// one bisection-tree level: node b is checked (res[b] = FE(node[b]) == 1, ++*nchecks) when parent is null or
+// parent[b / pdiv] == 0, else res[b] = 1 (bls_fe.hip k_fe_check_gated)
+hipError_t launch_final_check_gated(hipStream_t st, const Fp12* node, size_t n, const int* parent, uint32_t pdiv,
+                                    int* res, uint32_t* nchecks);
+// the same on the six-wave kernel (k_fe_wide)
+hipError_t launch_fe_wide_gated(hipStream_t st, const Fp12* node, size_t n, const int* parent, uint32_t pdiv, int* res,
+                                uint32_t* nchecks);
+// out[b] = prod_{i in [b chunk, (b + 1) chunk) and < n} a[i] b[i]
+hipError_t launch_fp12_chunk_prod2(hipStream_t st, const Fp12* a, const Fp12* b, size_t n, int chunk, Fp12* out);
+// bisection fallback (bls_bisect.hip): the -G1 comb table (neg_g1_comb_entries() G1A), -r_i G1 in affine (tmp: B
+// projective scratch points), verdicts from the leaf results
+size_t neg_g1_comb_entries();
+hipError_t launch_neg_g1_comb_table(hipStream_t st, G1A* tab);
+hipError_t launch_neg_rg1(hipStream_t st, size_t B, const int* status, const uint64_t* rsc, const G1A* tab, G1P* tmp,
+                          G1A* out);
+hipError_t launch_verdicts_res(hipStream_t st, const int* status, const int* res, size_t B, uint8_t* out);
+// projective -> affine with one inversion per 8 items (k_g1_affine_b); status-0 items -> identity
+hipError_t launch_g1_affine(hipStream_t st, size_t B, const int* status, const G1P* Pj, G1A* out);
 // nsel independent checks: out[b] = (FE(f[sel[b]]) == 1)
 hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out);
 hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out);
@@ -96,11 +112,6 @@ hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const 
 hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out);
 // signature decode + subgroup check with one wave per signature (k_sig_validate semantics)
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
-// Miller loop in F2 layout: the line records of n pairs (one wave each), then f over npairs pairs' lines (one
-// workgroup of six waves; conjugated, tower layout)
-hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L);
-hipError_t launch_facc_wide(hipStream_t st, const uint32_t* L, int npairs, Fp12* out);
-size_t lines_wide_u32(size_t n);
 // S = sum_b 2^b U_b of the MSM's 64 bit-sums (packed projective, bls_msm.hip) on one 16-wave workgroup
 hipError_t launch_msm_weighted_wide(hipStream_t st, const Fp* U, G2A* out);
 // the whole Miller loop of npairs <= 2 pairs on one workgroup (line waves + six f waves): out = f (tower Fp12);

@@ -297,31 +297,6 @@ __global__ void __launch_bounds__(256) k_reg_pack(const G1A* a, const int* ok, s
   valid[i] = v ? 1 : 0;
 }
 
-// (4) bisection fallback (fav_bisect in bls_capi.hip).  Per item i the two
-//     pairs (r_i apk_i, H_i) and (-r_i G1, sigma_i): the product of their
-//     Miller values over any subset is that subset's random-linear-combination
-//     check, with the same r_i as the whole-batch check (e(-r_i G1, sigma_i) =
-//     e(-G1, r_i sigma_i)).  This kernel computes -r_i G1 and lays the pairs
-//     out for k_miller2_vm (2 pairs per accumulator -> one Fp12 per item).
-__global__ void __launch_bounds__(64) k_bisect_pairs(size_t B, const uint64_t* rsc, const int* status, const G1A* rP,
-                                                     const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2) {
-  size_t i = gtid();
-  if (i >= B) return;
-  const int st = status[i];
-  G1A ng{fp_zero(), fp_zero(), true};
-  if (st) {
-    G1A g = g1_generator();
-    g.y = fp_neg(g.y);
-    ng = jac_to_aff(jac_mul_u64(jac_from_aff(g), rsc[i]));
-  }
-  P2[2 * i] = rP[i];
-  P2[2 * i + 1] = ng;
-  Q2[2 * i] = H[i];
-  Q2[2 * i + 1] = sig[i];
-  st2[2 * i] = st;
-  st2[2 * i + 1] = st;
-}
-
 // (5) AggregateVerify batches (bls_aggregate_verify_batch).  Item b owns the
 //     n_b pairs (pk_bj, m_bj) at pair indices io[b] .. io[b+1] and one
 //     signature; its pairs are laid out at io[b] + b + j, followed by the
@@ -536,12 +511,6 @@ hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t
     LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
   else
     LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
-  return hipSuccess;
-}
-hipError_t launch_bisect_pairs(hipStream_t st, size_t B, const uint64_t* rsc, const int* status, const G1A* rP,
-                               const G2A* H, const G2A* sig, G1A* P2, G2A* Q2, int* st2) {
-  if (!B) return hipSuccess;
-  LAUNCH(k_bisect_pairs, nblk(B, 64), 64, st, B, rsc, status, rP, H, sig, P2, Q2, st2);
   return hipSuccess;
 }
 hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok,

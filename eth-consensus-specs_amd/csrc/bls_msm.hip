@@ -105,7 +105,8 @@ __global__ void __launch_bounds__(64) k_msm_bucketc(const uint32_t* off, const u
   const int t = blockIdx.x * 64 + threadIdx.x;
   const int pi = t >> 1;
   const bool hi = (t & 1) != 0;
-  if (pi >= MSM_NB * MSM_C) return;
+  // every lane reaches the fold's barriers: the grid covers the MSM_NB * MSM_C lane pairs exactly
+  static_assert((2 * MSM_NB * MSM_C) % 64 == 0 && MSM_C <= 32, "k_msm_bucketc: whole waves, chunks within a wave");
   const int b = pi / MSM_C, c = pi % MSM_C;
   P2 R{fp2_zero(), fp2_one(), fp2_zero()};
   const uint32_t end = off[b + 1];

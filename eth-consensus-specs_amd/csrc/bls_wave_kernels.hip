@@ -82,55 +82,6 @@ __global__ void __launch_bounds__(64, 3) k_miller_vm(const G1A* P, const G2A* Q,
   }
 }
 
-// ================================ Miller loop, 2 pairs per accumulator ==
-// Item region (WL_M2_*): f (12) | (T (6), P (2), Q (4)) x 2 | scratch.  One
-// output per group of two pairs: f_{2j} f_{2j+1} (conjugated, x < 0).  A
-// skipped pair (status 0, identity, or padding) runs with P = (0, 0) and
-// Q = the G2 generator: its lines are then constants in Fp2, which the final
-// exponentiation maps to 1.
-template <int G>
-__global__ void __launch_bounds__(64) k_miller2_vm(const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* fout) {
-  __shared__ Fd slots[WP_NCONST + G * WL_M2_STRIDE];
-  __shared__ int skip[2 * G];
-  const int lane = threadIdx.x;
-  const size_t grp0 = (size_t)blockIdx.x * G;
-  const size_t ngrp = (n + 1) / 2;
-  vm_load_consts(slots);
-  if (lane < 2 * G) {
-    const size_t i = 2 * grp0 + lane;
-    skip[lane] = i >= n || (ok && !ok[i]) || P[i].inf || Q[i].inf;
-  }
-  __syncthreads();
-  const int item0 = WP_NCONST;
-  for (int k = lane; k < 24 * G; k += 64) {  // per pair: T (6) P (2) Q (4)
-    const int g = k / 24, pk = (k % 24) / 12, j = k % 12;
-    const size_t i = 2 * (grp0 + g) + pk;
-    const bool sk = skip[2 * g + pk];
-    const G2A q = sk ? g2_generator() : Q[i];
-    Fp v = fp_zero();
-    if (j < 4) v = (j & 1) ? (j < 2 ? q.x.c1 : q.y.c1) : (j < 2 ? q.x.c0 : q.y.c0);
-    else if (j == 4) v = FP_ONE;
-    else if (j == 6) v = sk ? fp_zero() : fp_neg(P[i].x);
-    else if (j == 7) v = sk ? fp_zero() : P[i].y;
-    else if (j >= 8) v = (j & 1) ? (j < 10 ? q.x.c1 : q.y.c1) : (j < 10 ? q.x.c0 : q.y.c0);
-    slots[item0 + g * WL_M2_STRIDE + WL_M2_PAIR + WL_M2_PSTRIDE * pk + j] = fd_from_fp(v);
-  }
-  __syncthreads();
-  vm_run<G>(VM_PROG(M2_FIRST), slots, item0, WL_M2_STRIDE, nullptr);
-  if ((X_ABS >> 62) & 1ull) vm_run<G>(VM_PROG(M2_ADD), slots, item0, WL_M2_STRIDE, nullptr);
-  for (int b = 61; b >= 0; --b) {
-    vm_run<G>(VM_PROG(M2_DBL), slots, item0, WL_M2_STRIDE, nullptr);
-    if ((X_ABS >> b) & 1ull) vm_run<G>(VM_PROG(M2_ADD), slots, item0, WL_M2_STRIDE, nullptr);
-  }
-  for (int k = lane; k < 12 * G; k += 64) {
-    const int g = k / 12, j = k % 12;
-    if (grp0 + g >= ngrp) continue;
-    Fp v = fp_from_fd(slots[item0 + g * WL_M2_STRIDE + WL_M2_F + j]);
-    if ((j >> 1) & 1) v = fp_neg(v);
-    fp12_slot_dst(fout[grp0 + g], j) = v;
-  }
-}
-
 // Products of consecutive chunks: out[b] = prod in[b*chunk .. min(n, (b+1)*chunk))
 __global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n, int chunk, Fp12* outp) {
   __shared__ Fd s[WP_NCONST + WL_CH_STRIDE];
@@ -141,6 +92,27 @@ __global__ void __launch_bounds__(64) k_fp12_chunk_prod(const Fp12* in, size_t n
   load_fp12(s + base, in + lo);
   for (size_t i = lo + 1; i < hi; i++) {
     load_fp12(s + base + 12, in + i);
+    vm_run<1>(VM_PROG(CH_MUL), s, base, 0, nullptr);
+  }
+  if (threadIdx.x < 12) fp12_slot_dst(outp[blockIdx.x], threadIdx.x) = fp_from_fd(s[base + threadIdx.x]);
+}
+
+// Products of consecutive chunks of pairwise products: out[b] = prod_{i in chunk b} a[i] b[i] (the bisection
+// tree's leaves, chunk = 1: an item's two Miller values, bls_capi.hip fav_bisect)
+__global__ void __launch_bounds__(64) k_fp12_chunk_prod2(const Fp12* a, const Fp12* b, size_t n, int chunk,
+                                                          Fp12* outp) {
+  __shared__ Fd s[WP_NCONST + WL_CH_STRIDE];
+  const size_t lo = (size_t)blockIdx.x * chunk;
+  const size_t hi = lo + chunk < n ? lo + chunk : n;
+  vm_load_consts(s);
+  const int base = WP_NCONST;
+  load_fp12(s + base, a + lo);
+  for (size_t i = lo; i < hi; i++) {
+    if (i != lo) {
+      load_fp12(s + base + 12, a + i);
+      vm_run<1>(VM_PROG(CH_MUL), s, base, 0, nullptr);
+    }
+    load_fp12(s + base + 12, b + i);
     vm_run<1>(VM_PROG(CH_MUL), s, base, 0, nullptr);
   }
   if (threadIdx.x < 12) fp12_slot_dst(outp[blockIdx.x], threadIdx.x) = fp_from_fd(s[base + threadIdx.x]);
@@ -173,18 +145,16 @@ hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const 
   return hipGetLastError();
 }
 
-// (n + 1) / 2 outputs; the product of all of them equals (after the final
-// exponentiation) the product of the n pairings.
-hipError_t launch_miller2(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f) {
-  if (!n) return hipSuccess;
-  const size_t ngrp = (n + 1) / 2;
-  hipLaunchKernelGGL(k_miller2_vm<2>, dim3((unsigned)((ngrp + 1) / 2)), dim3(64), 0, st, P, Q, ok, n, f);
-  return hipGetLastError();
-}
-
 hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_fp12_chunk_prod, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, in, n, chunk, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fp12_chunk_prod2(hipStream_t st, const Fp12* a, const Fp12* b, size_t n, int chunk, Fp12* out) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_chunk_prod2, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, a, b, n, chunk,
+                     out);
   return hipGetLastError();
 }
 

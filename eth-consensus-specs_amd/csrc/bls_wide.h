@@ -187,8 +187,10 @@ template <uint32_t KM>
 __device__ __forceinline__ uint32_t wmuls(uint32_t a) {
   if constexpr (KM <= 7u)
     return wnorm(a * KM);
-  else
-    return wmuls<KM / 2>(wmuls<2>(a)) + (KM & 1u ? a : 0u);  // KM even only on the paths used (8, 12, ...)
+  else if constexpr ((KM & 1u) == 0u)
+    return wmuls<KM / 2>(wmuls<2>(a));
+  else  // the sum of two normalised values is normalised again before it can enter a product
+    return wnorm(wmuls<KM / 2>(wmuls<2>(a)) + a);
 }
 
 // ---- conversions (kernel edges; lane-local work, not on the chain) ----------

@@ -542,27 +542,7 @@ struct LineW {
   }
 };
 
-__global__ void __launch_bounds__(64) k_lines_wide(const G1A* P, const G2A* Q, const int* ok, size_t n,
-                                                   uint32_t* L) {
-  const size_t i = blockIdx.x;
-  if (i >= n) return;
-  const WKG K = wkg_init();
-  const int lane = wlane();
-  LineW T;
-  T.init(P[i], Q[i], (!ok || ok[i]) && !P[i].inf && !Q[i].inf);
-  uint32_t* o = L + (size_t)i * MLW_STEPS * 3 * 64 + lane;
-#pragma unroll 1
-  for (int b = 62; b >= 0; --b) {
-    T.dbl(K, o);
-    o += 3 * 64;
-    if ((X_ABS >> b) & 1ull) {
-      T.add(K, o);
-      o += 3 * 64;
-    }
-  }
-}
-
-// f accumulation: six waves, wave k owns the w^k coefficient of f (w-basis: w^6 = xi; w^2k is c0.c_k, w^(2k+1)
+// f accumulation (k_miller_wide below): six waves, wave k owns the w^k coefficient of f (w-basis: w^6 = xi; w^2k is c0.c_k, w^(2k+1)
 // is c1.c_k of the tower).  f lives in LDS in F2 layout; a squaring or line product reads the operands of each of
 // the wave's products from LDS, so the per-wave term tables need no register indexing.
 //   f^2:  c_k = sum_{i+j=k} a_i a_j + xi sum_{i+j=k+6} a_i a_j   (3-4 products per wave)
@@ -577,62 +557,7 @@ __constant__ uint8_t FSQ_TERMS[6][4][4] = {  // (i, j, multiplier, xi) ; multipl
     {{0, 4, 2, 0}, {1, 3, 2, 0}, {2, 2, 1, 0}, {5, 5, 1, 1}},
     {{0, 5, 2, 0}, {1, 4, 2, 0}, {2, 3, 2, 0}, {0, 0, 0, 0}}};
 
-__global__ void __launch_bounds__(384) k_facc_wide(const uint32_t* L, int npairs, Fp12* out) {
-  __shared__ uint32_t fs[6 * 64];
-  const WKG K = wkg_init();
-  const int lane = wlane(), k = (int)(threadIdx.x >> 6);
-  const uint32_t kn = K.kneg;
-  fs[k * 64 + lane] = k == 0 ? wf_from_fp2(fp2_one()) : 0u;
-  __syncthreads();
-  int step = 0;
-#pragma unroll 1
-  for (int b = 62; b >= 0; --b) {
-    if (b != 62) {  // f = f^2
-      uint32_t plain = 0, xs = 0;
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const uint32_t ii = FSQ_TERMS[k][t][0], jj = FSQ_TERMS[k][t][1], m = FSQ_TERMS[k][t][2];
-        const uint32_t pr = wf_mul(kn, fs[ii * 64 + lane], fs[jj * 64 + lane]);
-        const uint32_t pm = wnorm(pr * m);
-        if (FSQ_TERMS[k][t][3]) xs = wadd(xs, pm); else plain = wadd(plain, pm);
-      }
-      const uint32_t c = wadd(plain, wf_xi(K.k1, xs));
-      __syncthreads();
-      fs[k * 64 + lane] = c;
-      __syncthreads();
-    }
-    const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
-#pragma unroll 1
-    for (int sl = 0; sl < nl; ++sl, ++step) {
-#pragma unroll 1
-      for (int pi = 0; pi < npairs; ++pi) {
-        const uint32_t* l = L + ((size_t)pi * MLW_STEPS + step) * 3 * 64 + lane;
-        const uint32_t l0 = l[0], l2 = l[64], l3 = l[128];
-        const int i2 = (k + 4) % 6, i3 = (k + 3) % 6;
-        const uint32_t p0 = wf_mul(kn, fs[k * 64 + lane], l0);
-        const uint32_t p2 = wf_mul(kn, fs[i2 * 64 + lane], l2);
-        const uint32_t p3 = wf_mul(kn, fs[i3 * 64 + lane], l3);
-        const uint32_t xw = wadd(k < 2 ? p2 : 0u, k < 3 ? p3 : 0u);
-        const uint32_t pl = wadd(p0, wadd(k < 2 ? 0u : p2, k < 3 ? 0u : p3));
-        const uint32_t c = wadd(pl, wf_xi(K.k1, xw));
-        __syncthreads();
-        fs[k * 64 + lane] = c;
-        __syncthreads();
-      }
-    }
-  }
-  // x < 0: conjugate (negate the odd w-coefficients); canonical Fp2 into the tower slot of w^k
-  const uint32_t c = fs[k * 64 + lane];
-  const uint32_t neg = (k & 1) ? wnorm(K.k1024 - c) : c;  // -c on both halves (c < 100p)
-  const Fp2 v = wf_to_fp2(neg);
-  if (lane == 0) {
-    Fp6& h6 = (k & 1) ? out->c1 : out->c0;
-    Fp2& dst = (k >> 1) == 0 ? h6.c0 : ((k >> 1) == 1 ? h6.c1 : h6.c2);
-    dst = v;
-  }
-}
-
-// Fused per-call Miller loop: waves 0..5 accumulate f (as k_facc_wide, each f^2 and f l as ONE reduction of
+// Fused per-call Miller loop: waves 0..5 accumulate f (each f^2 and f l as ONE reduction of
 // lazily summed products, f ping-ponging between two LDS banks), wave 6 + p runs pair p's G2 side (LineW) and
 // writes its line records into LDS.  The two sides meet through per-pair progress counters (release / acquire at
 // workgroup scope); the six f waves synchronise among themselves through a counter barrier, since the line waves
@@ -738,17 +663,6 @@ hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const 
   hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out);
   return hipGetLastError();
 }
-
-hipError_t launch_lines_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, uint32_t* L) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_lines_wide, dim3((unsigned)n), dim3(64), 0, st, P, Q, ok, n, L);
-  return hipGetLastError();
-}
-hipError_t launch_facc_wide(hipStream_t st, const uint32_t* L, int npairs, Fp12* out) {
-  hipLaunchKernelGGL(k_facc_wide, dim3(1), dim3(384), 0, st, L, npairs, out);
-  return hipGetLastError();
-}
-size_t lines_wide_u32(size_t n) { return n * (size_t)MLW_STEPS * 3 * 64; }
 
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad) {
   if (!nw) return hipSuccess;

@@ -184,9 +184,10 @@ int bls_gt_mul(bls_ctx* ctx, const uint8_t* a576, const uint8_t* b576, uint8_t* 
  * :229): subgroup_check 0 skips the subgroup checks of bls_pairing_check. */
 int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, int subgroup_check);
 
-/* Fallback statistics of the last batch call on this context: the number of
- * batched final-exponentiation checks and bisection rounds it ran (both 0
- * when the whole-batch check passed).  Returns 0 or BLS_E_*. */
+/* Fallback statistics of the last batch finished on this context: the number
+ * of final-exponentiation checks and bisection rounds (tree levels) it ran
+ * (both 0 when the whole-batch check passed; waits for that batch's
+ * verdicts).  Returns 0 or BLS_E_*. */
 int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds);
 
 /* Synthetic registry for benchmarks: pk_i = (first_sk + i) * G1 written
@@ -202,6 +203,8 @@ int bls_sk_to_pk_batch(bls_ctx* ctx, const uint8_t* sks32, size_t B, uint8_t* ou
 void* bls_dev_alloc(bls_ctx* ctx, size_t bytes);
 int bls_dev_free(bls_ctx* ctx, void* dptr);
 int bls_h2d(bls_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* bls_d2h and bls_sync first wait for every job stream of the context (verdicts
+ * of pipelined jobs are written asynchronously, see bls_fav_job_finish_dev). */
 int bls_d2h(bls_ctx* ctx, void* dst, const void* src, size_t bytes);
 int bls_sync(bls_ctx* ctx);
 
@@ -232,7 +235,10 @@ int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out);
  *   partial: wait for the job's 576-byte Miller product
  *   check:   final exponentiation of the product of n partials on the job's
  *            stream: 1 / 0
- *   finish:  verdicts into d_out (bisection when batch_ok == 0); waits */
+ *   finish:  verdicts into d_out, enqueued on the job's stream without a host
+ *            wait -- a failing batch's bisection runs there on the device (no
+ *            host round trip per round) while the host checks the next job;
+ *            bls_d2h / bls_sync wait for it */
 int bls_fav_job_submit_dev(bls_ctx* ctx, int job, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
                            const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32);
 int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576);

@@ -80,3 +80,79 @@ def test_two_rank_partials(tamper):
     for p in procs:
         p.join(timeout=60)
     assert res == {0: (not tamper, True), 1: (not tamper, not tamper)}  # only rank 1's shard is bad
+
+
+# ---- shards balanced by work (contiguous blocks of aggregates, balanced by
+# total pubkey count).  Electra aggregates carry up to MAX_VALIDATORS_PER_COMMITTEE * MAX_COMMITTEES_PER_SLOT =
+# 2,048 * 64 = 131,072 indices (specs/electra/beacon-chain.md:365), beside committees of a few hundred.
+ELECTRA_SIZES = [131072, 64, 2048, 512, 3, 131072 // 2, 1, 2047] * 4 + [512] * 40
+
+
+def _check_partition(bounds, offs, per_item, world):
+    from bls_mi355x.dist import ITEM_WORK_KEYS  # noqa: F401  (the default weight is the §8(d) model's)
+
+    B = len(offs) - 1
+    assert bounds[0][0] == 0 and bounds[-1][1] == B
+    assert all(bounds[r][1] == bounds[r + 1][0] for r in range(world - 1))
+    work = [int(offs[hi] - offs[lo]) + per_item * (hi - lo) for lo, hi in bounds]
+    item_max = max(int(offs[i + 1] - offs[i]) for i in range(B)) + per_item
+    total = sum(work)
+    assert all(abs(w - total / world) <= item_max for w in work), (work, total / world, item_max)
+    return work
+
+
+def test_shard_bounds_by_work_balances_variable_committees():
+    import numpy as np
+
+    from bls_mi355x.dist import ITEM_WORK_KEYS, shard_bounds, shard_bounds_by_work
+
+    for sizes in (ELECTRA_SIZES, [512] * 2048, [1] * 1000 + [131072], list(range(1, 300))):
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        for world in (1, 2, 3, 4, 8):
+            for per_item in (0, ITEM_WORK_KEYS):
+                bounds = [shard_bounds_by_work(offs, r, world, per_item) for r in range(world)]
+                _check_partition(bounds, offs, per_item, world)
+    # uniform committees: the same blocks as the item-count split
+    offs = np.arange(2049) * 512
+    assert [shard_bounds_by_work(offs, r, 8) for r in range(8)] == [shard_bounds(2048, r, 8) for r in range(8)]
+    # the item-count split is what the work split fixes: one rank would hold both 131,072-key aggregates
+    offs = np.concatenate([[0], np.cumsum(ELECTRA_SIZES)])
+    naive = [shard_bounds(len(ELECTRA_SIZES), r, 8) for r in range(8)]
+    naive_work = [int(offs[hi] - offs[lo]) for lo, hi in naive]
+    assert max(naive_work) > 4 * min(naive_work)
+
+
+def _balance_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+
+    from bls_mi355x.dist import ITEM_WORK_KEYS, shard_bounds_by_work
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    offs = np.concatenate([[0], np.cumsum(ELECTRA_SIZES)])
+    mine = shard_bounds_by_work(offs, rank, world)  # each rank from the same offsets, no exchange of bounds
+    allb = [None] * world
+    dist.all_gather_object(allb, (rank, mine))
+    q.put((rank, sorted(allb), ITEM_WORK_KEYS))
+    dist.destroy_process_group()
+
+
+def test_two_rank_electra_shards():
+    """world 2 over gloo: the ranks' independently computed blocks partition the batch, balanced by work."""
+    import numpy as np
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balance_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (b, w)) for r, b, w in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][0] == res[1][0]
+    bounds = [b for _, b in res[0][0]]
+    offs = np.concatenate([[0], np.cumsum(ELECTRA_SIZES)])
+    _check_partition(bounds, offs, res[0][1], 2)

@@ -6,6 +6,8 @@ batches).  Verdicts are known by construction and cross-checked on small
 cases with the C oracle (oracle/bls_oracle.c).  Requires an MI355X."""
 import hashlib
 
+import linecache
+
 import numpy as np
 import pytest
 
@@ -156,8 +158,11 @@ def apply_deposit(shim, pk, m, sig, registry):          # specs/phase0/beacon-ch
 
 
 def _block_fns():
+    # with readable source lines, as the generated spec modules have them (sigsets reads the assert sites)
+    linecache.cache["<generated block spec>"] = (len(BLOCK_SRC), None, BLOCK_SRC.splitlines(True),
+                                                 "<generated block spec>")
     ns = {}
-    exec(compile(BLOCK_SRC, "<generated spec>", "exec"), ns)
+    exec(compile(BLOCK_SRC, "<generated block spec>", "exec"), ns)
     return ns
 
 

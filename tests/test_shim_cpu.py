@@ -151,3 +151,47 @@ def test_rlc_seed_fails_closed(tmp_path):
         assert lib.bls_host_seed(buf) == 0
         seeds.add(buf.raw)
     assert len(seeds) == 4
+
+
+def test_integration_patch_imports_without_wheels(monkeypatch):
+    """the reference-side patch of INTEGRATION.md §1 must import where milagro, arkworks and
+    py_ecc are absent (the MI355X box).  Executes the two python blocks of §1 -- the guarded imports replacing
+    E/utils/bls.py:1-53 and the use_mi355x switch -- with those wheels made unimportable, between them the
+    fastest_bls class as the patch describes it (E/utils/bls.py:57-68 with mi355x_bls for milagro_bls)."""
+    import builtins
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "INTEGRATION.md")) as fh:
+        text = fh.read()
+    sec = text[text.index("## 1."):text.index("## 2.")]
+    blocks = re.findall(r"```python\n(.*?)```", sec, re.S)
+    assert len(blocks) == 3  # (a) guarded imports, (b) the switch, then the conftest choice
+    monkeypatch.setenv("BLSMI355X_HOME", os.path.join(root, "eth-consensus-specs_amd"))
+    real_import = builtins.__import__
+
+    def no_wheels(name, *a, **kw):
+        if name.split(".")[0] in ("milagro_bls_binding", "py_arkworks_bls12381", "py_ecc"):
+            raise ImportError(f"No module named {name!r}")
+        return real_import(name, *a, **kw)
+
+    monkeypatch.setattr(builtins, "__import__", no_wheels)
+    monkeypatch.setattr(sys, "path", list(sys.path))
+    ns = {"__name__": "eth2spec_utils_bls_patched"}
+    exec(compile(blocks[0], "<INTEGRATION §1a>", "exec"), ns)
+    assert ns["milagro_bls"] is None and ns["arkworks_bls"] is None and ns["py_ecc_bls"] is None
+    assert ns["BLS_MODULUS"] == 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    fastest = ("class fastest_bls:\n" + "".join(
+        f"    {n} = {v}\n" for n, v in (("G1", "arkworks_G1"), ("G2", "arkworks_G2"), ("Scalar", "arkworks_Scalar"),
+                                       ("GT", "arkworks_GT"))) + "".join(
+        f"    {n} = mi355x_bls.{n}\n" for n in ("_AggregatePKs", "Sign", "Verify", "Aggregate", "AggregateVerify",
+                                               "FastAggregateVerify", "SkToPk")) + "bls = fastest_bls\n")
+    exec(compile(fastest, "<E/utils/bls.py:57-76>", "exec"), ns)
+    exec(compile(blocks[1], "<INTEGRATION §1b>", "exec"), ns)
+    from bls_mi355x import curve
+    from bls_mi355x.backend import mi355x_bls
+
+    assert callable(ns["use_mi355x"]) and ns["bls"] is ns["fastest_bls"]
+    assert ns["bls"].FastAggregateVerify is mi355x_bls.FastAggregateVerify
+    assert ns["arkworks_G1"] is curve.G1Point and ns["Scalar"] is curve.Scalar
+    assert ns["py_ecc_Scalar"](5).inverse() * 5 == 1

@@ -2,8 +2,19 @@
 recording through the shim, routing of each set, stub mode and exception
 handling -- no device call (the batch executors are replaced by fakes that
 record what they were asked)."""
+import linecache
+
 import numpy as np
 import pytest
+
+
+def compile_spec(src: str, name: str) -> dict:
+    """Compile spec-shaped source the way the generated pyspec modules exist -- with readable source lines
+    (linecache, as a module file provides them): sigsets.result_is_asserted reads the caller's source."""
+    linecache.cache[name] = (len(src), None, src.splitlines(True), name)
+    ns = {}
+    exec(compile(src, name, "exec"), ns)
+    return ns
 
 
 class FakeRegistry:
@@ -91,8 +102,7 @@ def _apply_deposit(shim, pk, m, sig, applied):  # specs/phase0/beacon-chain.md:2
 def _compare(shim, pk, m, sig):
     return shim.Verify(pk, m, sig) is False
 """
-_spec = {}
-exec(compile(SPEC_SRC, "<generated spec>", "exec"), _spec)
+_spec = compile_spec(SPEC_SRC, "<generated spec>")
 _process_randao = _spec["_process_randao"]
 _process_attestation = _spec["_process_attestation"]
 _process_av = _spec["_process_av"]
@@ -143,23 +153,38 @@ def test_deferred_branching_site_gets_the_real_verdict(fakes, monkeypatch):
     assert len(col) == 0 and col.eager == 3 and col.results == []
 
 
-def test_deferred_counts_version_fallback(fakes, monkeypatch):
-    """on an interpreter other than 3.10 nothing can be deferred; the collector must count those
-    calls (version_fallback) and warn once instead of silently losing the batching."""
+def test_deferred_is_interpreter_independent(fakes, monkeypatch):
+    """the assert-site analysis reads source, not bytecode, so the reference's supported
+    interpreters (pyproject.toml:10, >=3.10 <3.14) all batch the asserted calls (nothing keyed on the version)."""
+    sigsets, calls = fakes
+    from bls_mi355x import bls as shim
+
+    keys = [_pk(i) for i in range(2)]
+    shim.bls_active = True
+    for ver in ((3, 11, 9, "final", 0), (3, 12, 0, "final", 0), (3, 13, 1, "final", 0)):
+        monkeypatch.setattr(sigsets.sys, "version_info", ver)
+        with sigsets.deferred(FakeRegistry(keys), check=False) as col:
+            _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
+            _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
+        assert len(col) == 2 and col.eager == 0 and col.results == [True, True]
+    assert not hasattr(sigsets.SignatureSets(None), "version_fallback")
+
+
+def test_deferred_without_source_runs_at_once(fakes, monkeypatch):
+    """A caller whose source cannot be read (no file, not in linecache) gets the real verdict at once."""
     sigsets, _ = fakes
     from bls_mi355x import bls as shim
     from bls_mi355x.backend import mi355x_bls
 
     monkeypatch.setattr(mi355x_bls, "FastAggregateVerify", staticmethod(lambda pks, m, s: True))
     monkeypatch.setattr(shim.fastest_bls, "FastAggregateVerify", mi355x_bls.FastAggregateVerify)
-    keys = [_pk(i) for i in range(2)]
+    ns = {}
+    exec(compile("def f(shim, k):\n    assert shim.FastAggregateVerify(k, b'\\x03' * 32, b'\\x04' * 96)\n",
+                 "<no source>", "exec"), ns)
     shim.bls_active = True
-    monkeypatch.setattr(sigsets.sys, "version_info", (3, 12, 0, "final", 0))
-    with pytest.warns(RuntimeWarning, match="3.10 bytecode"):
-        with sigsets.deferred(FakeRegistry(keys), check=False) as col:
-            _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
-            _process_attestation(shim, keys, b"\x03" * 32, b"\x04" * 96)
-    assert len(col) == 0 and col.eager == 2 and col.version_fallback == 2
+    with sigsets.deferred(FakeRegistry([_pk(0)]), check=False) as col:
+        ns["f"](shim, [_pk(0)])
+    assert len(col) == 0 and col.eager == 1
 
 
 PATTERNS_SRC = """
@@ -216,12 +241,40 @@ def nested_arg(f):
 
 def in_conditional(c):
     assert (probe() if c else False) or True
+
+
+def multi_line_assert():
+    assert probe(
+    ), (
+        "message"
+    )
+
+
+def multi_line_return():
+    return (
+        probe()
+    )
+
+
+def through_multi_line():
+    assert multi_line_return()
+
+
+def same_line_mixed():
+    assert probe() or not probe()
+
+
+def in_lambda():
+    assert not (lambda: probe())()
+
+
+def in_comprehension():
+    assert not [probe() for _ in [0]][0]
 """
 
 
-def test_result_is_asserted_bytecode_patterns():
-    ns = {}
-    exec(compile(PATTERNS_SRC, "<patterns>", "exec"), ns)
+def test_result_is_asserted_patterns():
+    ns = compile_spec(PATTERNS_SRC, "<patterns>")
     ns["asserted"]()
     ns["asserted_msg"]()
     ns["through_return"]()
@@ -231,24 +284,11 @@ def test_result_is_asserted_bytecode_patterns():
     ns["via_sorted"]()
     ns["nested_arg"](lambda v: v is False)  # probe() is an argument of f, not the asserted call
     ns["in_conditional"](True)
-
-
-def test_callee_name_reads_the_call():
-    import dis
-    import sys as _sys
-
-    from bls_mi355x.sigsets import callee_name
-
-    if _sys.version_info[:2] != (3, 10):
-        pytest.skip("bytecode simulation is for Python 3.10")
-
-    ns = {}  # compiled from source: pytest rewrites this module's asserts
-    exec(compile("def f(bls, x, g):\n    assert bls.Verify(x, g(x), 3)\n    return any(map(bls.Verify, x))\n",
-                 "<f>", "exec"), ns)
-    f = ns["f"]
-    calls = [i for i in dis.get_instructions(f) if i.opname.startswith("CALL_")]
-    names = [callee_name(f.__code__, c.offset) for c in calls]
-    assert names == ["g", "Verify", "map", "any"]
+    ns["multi_line_assert"]()
+    ns["through_multi_line"]()
+    ns["same_line_mixed"]()  # one of the line's calls is negated: neither is deferred
+    ns["in_lambda"]()
+    ns["in_comprehension"]()
 
 
 def test_wrong_lengths_are_false_not_errors(fakes):
