@@ -92,6 +92,14 @@ C3_SLOTS, C3_PER_SLOT, C3_N = 32, 64, 512  # presets/mainnet/phase0.yaml: SLOTS_
 C4_TOTAL, C4_CHUNK = 10 ** 6, 125_000
 
 
+def launch_grid(kernel: str, items: int) -> int | None:
+    """Threads of one launch of the roofline kernel over `items` FAV items (rocprofv3's grid_x): k_miller_acc4q<2>
+    runs 4 lanes per two pairs, k_miller_lines2 2 lanes per pair, k_fav_gather_q<16> 16 lanes per aggregate;
+    64-lane workgroups (bls_miller_pair.hip, bls_miller_lane.hip, bls_kernels.hip)."""
+    lanes = {"miller": 4 * ((items + 1) // 2), "miller_lines": 2 * items, "fav_gather": 16 * items}.get(kernel)
+    return None if lanes is None else (lanes + 63) // 64 * 64
+
+
 def model_fme(n: int):
     """Per-item algorithmic work of FAV(n) with a resident registry."""
     return {
@@ -676,12 +684,18 @@ def main():
                                f"one-batch-at-a-time passes after the timed region)",
                 "traffic": traffic, "traffic_source": tsrc, "ops_per_launch": ops,
                 "avg_launch_ms": round(avg_s * 1e3, 4)}
-        try:  # the committed rocprofv3 --kernel-trace --stats average of the same kernel -- only for the same build
+        try:  # the committed rocprofv3 --kernel-trace --stats average of the same kernel, launched at THIS size
+            # (the (symbol, grid) entry: a C2-only, one-batch-at-a-time profile, tools/gpu_check.sh profc2) -- only
+            # for the same build
             with open(ROCPROF_AVG) as fh:
                 rj = json.load(fh)
-            r_ms = rj["avg_ms"].get(KERNEL_SYMBOL.get(dom))
-            if r_ms and rj.get("lib_sha256_16") and rj["lib_sha256_16"] == _lib_sha():
+            grid = launch_grid(dom, per_launch)
+            ent = rj.get("avg_ms_by_grid", {}).get(KERNEL_SYMBOL.get(dom), {}).get(str(grid))
+            if ent and rj.get("lib_sha256_16") and rj["lib_sha256_16"] == _lib_sha():
+                r_ms = ent["avg_ms"]
                 roof["rocprof_avg_ms"] = r_ms
+                roof["rocprof_grid"] = grid
+                roof["rocprof_calls"] = ent["calls"]
                 roof["rocprof_source"] = rj["source"] + " (committed profile of this exact libblsmi355x.so)"
                 roof["frac_rocprof"] = round(ops / (r_ms * 1e-3) / PEAK_INT_OPS, 5)
         except (OSError, ValueError, KeyError):

@@ -10,11 +10,11 @@ import ctypes
 import os
 import threading
 
-HW_QUEUES = 24  # 7 FAV jobs x 3 streams share them with the default/copy streams (7:24 measured best)
+HW_QUEUES = 24  # 10 FAV jobs x 2 streams + the fallback stream share them with the default/copy streams
 
 
 def hw_queue_policy() -> None:
-    """The library keeps up to BLS_FAV_JOBS_INIT x 3 streams busy; with HIP's default of 4 hardware queues per
+    """The library keeps up to BLS_FAV_JOBS_INIT x BLS_JOB_STREAMS streams busy; with HIP's default of 4 hardware queues per
     process, streams share queues and a long one-lane-per-item kernel blocks every kernel queued behind it
     (measured: 687k -> 838k FAV/s at 8+ queues; 5 jobs: 1.00M at 16, 1.02M at 20).  HIP reads
     GPU_MAX_HW_QUEUES once, when it starts, so this sets it at import -- only when the variable is unset (an
@@ -85,6 +85,7 @@ _SIGS = {
     "bls_fav_job_submit_dev": (_ip, [_vp, _ip, _vp, _vp, _sz, _vp, _vp, _u8p]),
     "bls_fav_job_partial": (_ip, [_vp, _ip, _vp]),
     "bls_fav_job_check": (_ip, [_vp, _ip, _u8p, _sz]),
+    "bls_fav_job_check_own": (_ip, [_vp, _ip]),
     "bls_fav_job_finish_dev": (_ip, [_vp, _ip, _ip, _vp]),
     "bls_registry_generate": (_ip, [_vp, ctypes.c_uint64, _sz, _vp]),
     "bls_last_fallback_stats": (_ip, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),

@@ -17,11 +17,11 @@ import numpy as np
 
 from . import _native
 
-# per-context job slots with streams: BLS_FAV_JOBS_INIT (default 7 with 24 hardware queues: the round-4 sweeps,
-# profiles/r04e_jobs_sweep.txt and r04o2_jobs_ab.txt -- 7:24 beats 6:24 by ~1 % on C2 and ~3 % on C3, 7:28 and
-# 8:32 are slower) of the
-# BLS_FAV_JOBS = 8 in include/blsmi355x.h, read by the library at bls_ctx_create
-FAV_JOBS = max(1, min(8, int(os.environ.get("BLS_FAV_JOBS_INIT", "7"))))
+# per-context job slots with streams: BLS_FAV_JOBS_INIT (default 10: two streams per job, the batch checks on the
+# jobs' own streams, 21 of the 24 hardware queues -- profiles/r05h_jobs_streams_ab.txt: C2 +3 %, C3 +13 % over 7
+# three-stream jobs with one shared FE stream; 11 jobs and more, or more streams than queues, collapse) of the
+# BLS_FAV_JOBS = 16 in include/blsmi355x.h, read by the library at bls_ctx_create
+FAV_JOBS = max(1, min(16, int(os.environ.get("BLS_FAV_JOBS_INIT", "10"))))
 # batches kept in flight by run_pipelined (<= FAV_JOBS)
 FAV_DEPTH = max(1, min(FAV_JOBS, int(os.environ.get("BLS_FAV_DEPTH", str(FAV_JOBS)))))
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001  # the BLS12-381 group order r
@@ -388,6 +388,11 @@ class ResidentFavBatch:
         c = self.ctx
         return c.check(c.lib.bls_fav_job_check(c.h, job, partials, len(partials) // 576)) == 1
 
+    def job_check_own(self, job: int) -> bool:
+        """The job's own product alone (bls_fav_job_check_own: the check submit enqueued behind it)."""
+        c = self.ctx
+        return c.check(c.lib.bls_fav_job_check_own(c.h, job)) == 1
+
     def job_finish(self, job: int, batch_ok: bool, chunk: int = 0) -> None:
         c = self.ctx
         lo = self._chunk_ptrs(chunk)[3]
@@ -419,9 +424,11 @@ class ResidentFavBatch:
             job = u % FAV_JOBS
             if comm:
                 ok = self.job_check_comm(job)
+            elif exchange is None:  # one shard: its own check, already enqueued behind its product
+                ok = self.job_check_own(job)
             else:
                 part = self.job_partial(job)
-                ok = self.job_check(job, exchange(part) if exchange else part)
+                ok = self.job_check(job, exchange(part))
             self.job_finish(job, ok, ch)
             oks[k] = oks[k] and ok
             if u + depth < len(units):

@@ -21,7 +21,7 @@ namespace {
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
   // FAV batch state (kept between partial and finish)
-  S_FAV_F, S_FAV_FT, S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_SAFF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
+  S_FAV_F, S_FAV_FT, S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
   S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD, S_BSIG, S_BRSC, S_BLINES,
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
@@ -36,6 +36,7 @@ enum Slot {
   // per-call Verify / FastAggregateVerify pair points (not S_RP: a FAV batch's r_i apk_i live there between its
   // partial and finish calls, and fav_bisect reads them back)
   S_PC_P,
+  S_OWN,  // the job's own final check (job_submit)
   NSLOT
 };
 
@@ -68,7 +69,12 @@ struct Job {
   size_t fav_B = 0;
   bool fav_ready = false;
   bool partial_pending = false;
-  bool own_check_failed = false;  // the last check of this job was of its own partial alone, and it failed
+  // the final-exponentiation check of the job's own product, enqueued by job_submit right behind it:
+  // h_own[0] = its verdict once ev_own has passed; own_state -1 not read yet, 0 failed, 1 passed
+  int* h_own = nullptr;
+  hipEvent_t ev_own = nullptr;
+  bool own_pending = false;
+  int own_state = -1;
   int fav_mg = 1;  // pairs per f of the prepared batch's Miller accumulation
   // last bisection fallback: final-exponentiation checks and rounds (levels); the checks of a FAV bisection are
   // counted on the device (bis_dev_checks, read after the job's stream by bls_last_fallback_stats)
@@ -78,7 +84,7 @@ struct Job {
 
 struct bls_ctx {
   int device = 0;
-  int njobs = 7;  // job slots with streams: BLS_FAV_JOBS_INIT (default 7, at most BLS_FAV_JOBS)
+  int njobs = 10;  // job slots with streams: BLS_FAV_JOBS_INIT (default 10, at most BLS_FAV_JOBS)
   Job jobs[BLS_FAV_JOBS];
   Job* j = &jobs[0];  // the job the current call works on
   std::mutex mu;
@@ -265,14 +271,18 @@ int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
   int* d_r;
   SCR(S_INT, 4, d_r);
   Job& J = *ctx->j;
-  HIPCK(hipEventRecord(J.ev_fe, J.stream));
-  HIPCK(hipStreamWaitEvent(ctx->fe_stream, J.ev_fe, 0));
+  // the context's FE stream, or the job's own (BLS_FE_STREAM=job: one hardware queue fewer)
+  hipStream_t fe = ctx->fe_stream ? ctx->fe_stream : J.stream;
+  if (fe != J.stream) {
+    HIPCK(hipEventRecord(J.ev_fe, J.stream));
+    HIPCK(hipStreamWaitEvent(fe, J.ev_fe, 0));
+  }
   // batch checks on the one-wave k_fe_check, which leaves the CU to the other jobs (profiles/r04m_fe_ab.txt: 1.92 M vs
   // 1.84 M FAV/s with every check six-wave); the per-call path runs k_fe_wide on its own stream (verify_percall)
-  PROF2(7, ctx->fe_stream, launch_final_check_wave(ctx->fe_stream, f, n, d_r));
+  PROF2(7, fe, launch_final_check_wave(fe, f, n, d_r));
   int r = 0;
-  HIPCK(hipMemcpyAsync(&r, d_r, sizeof r, hipMemcpyDeviceToHost, ctx->fe_stream));
-  HIPCK(hipStreamSynchronize(ctx->fe_stream));
+  HIPCK(hipMemcpyAsync(&r, d_r, sizeof r, hipMemcpyDeviceToHost, fe));
+  HIPCK(hipStreamSynchronize(fe));
   return r ? 1 : 0;
 }
 
@@ -282,9 +292,11 @@ int run_final_checks_sel(bls_ctx* ctx, const Fp12* f, const uint32_t* sel, size_
                          int* res) {
   if (!nsel) return 0;
   Job& J = *ctx->j;
-  hipStream_t fe = ctx->fe_stream;
-  HIPCK(hipEventRecord(J.ev_fe, J.stream));
-  HIPCK(hipStreamWaitEvent(fe, J.ev_fe, 0));
+  hipStream_t fe = ctx->fe_stream ? ctx->fe_stream : J.stream;
+  if (fe != J.stream) {
+    HIPCK(hipEventRecord(J.ev_fe, J.stream));
+    HIPCK(hipStreamWaitEvent(fe, J.ev_fe, 0));
+  }
   HIPCK(hipMemcpyAsync(d_sel, sel, 4 * nsel, hipMemcpyHostToDevice, fe));
   PROF2(8, fe, launch_final_check_sel(fe, f, d_sel, nsel, d_res));
   HIPCK(hipMemcpyAsync(res, d_res, 4 * nsel, hipMemcpyDeviceToHost, fe));
@@ -352,10 +364,16 @@ struct JobScope {
 
 extern "C" {
 
-static bool job_init(Job& J, int prio_hi) {
+// streams: 3, or 2 with stream3 an alias of stream2 (fav_prepare's two-stream order)
+static bool job_init(Job& J, int prio_hi, int streams) {
+  if (streams < 3) {
+    if (hipStreamCreateWithFlags(&J.stream2, hipStreamNonBlocking) != hipSuccess) return false;
+    J.stream3 = J.stream2;
+  } else if (hipStreamCreateWithFlags(&J.stream2, hipStreamNonBlocking) != hipSuccess ||
+             hipStreamCreateWithPriority(&J.stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+    return false;
+  }
   return hipStreamCreateWithFlags(&J.stream, hipStreamNonBlocking) == hipSuccess &&
-         hipStreamCreateWithFlags(&J.stream2, hipStreamNonBlocking) == hipSuccess &&
-         hipStreamCreateWithPriority(&J.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_fork, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_join, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_sig, hipEventDisableTiming) == hipSuccess &&
@@ -366,20 +384,23 @@ static bool job_init(Job& J, int prio_hi) {
          hipEventCreateWithFlags(&J.ev_fb, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_fe, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_bis, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_own, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc((void**)&J.h_own, 2 * sizeof(int), hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc((void**)&J.h_partial, 576, hipHostMallocDefault) == hipSuccess;
 }
 
 static void job_destroy(Job& J) {
-  hipStream_t ss[3] = {J.stream, J.stream2, J.stream3};
+  hipStream_t ss[3] = {J.stream, J.stream2, J.stream3 == J.stream2 ? nullptr : J.stream3};
   for (hipStream_t s : ss)
     if (s) (void)hipStreamSynchronize(s);
   for (auto& b : J.buf)
     if (b.p) (void)hipFree(b.p);
-  hipEvent_t es[10] = {J.ev_fork, J.ev_join, J.ev_sig,  J.ev_msm, J.ev_gather,
-                       J.ev_partial, J.ev_h2c, J.ev_fb, J.ev_fe, J.ev_bis};
+  hipEvent_t es[11] = {J.ev_fork,    J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial,
+                       J.ev_h2c, J.ev_fb,   J.ev_fe,  J.ev_bis, J.ev_own};
   for (hipEvent_t e : es)
     if (e) (void)hipEventDestroy(e);
   if (J.h_partial) (void)hipHostFree(J.h_partial);
+  if (J.h_own) (void)hipHostFree(J.h_own);
   for (hipStream_t s : ss)
     if (s) (void)hipStreamDestroy(s);
 }
@@ -398,14 +419,22 @@ int bls_ctx_create(int device, bls_ctx** out) {
   // All job streams are created here, before any kernel runs (streams created
   // later, between launches, were measured to hit HSA_STATUS_ERROR_OUT_OF_RESOURCES).
   if (const char* v = getenv("BLS_FAV_JOBS_INIT")) c->njobs = atoi(v) < 1 ? 1 : atoi(v) > BLS_FAV_JOBS ? BLS_FAV_JOBS : atoi(v);
+  // streams per job (BLS_JOB_STREAMS, default 2, or 3): with two, 10 jobs fit the hardware queues that held 7
+  // (profiles/r05h_jobs_streams_ab.txt: C2 +3 %, C3 +13 %)
+  int streams = 2;
+  if (const char* v = getenv("BLS_JOB_STREAMS")) streams = atoi(v) == 3 ? 3 : 2;
   for (int k = 0; k < c->njobs; ++k) {
-    if (!job_init(c->jobs[k], prio_hi)) {
+    if (!job_init(c->jobs[k], prio_hi, streams)) {
       bls_ctx_destroy(c);
       return BLS_E_DEVICE;
     }
   }
+  // batch checks on each job's own stream (default) or on one context-wide FE stream (BLS_FE_STREAM=ctx): on one
+  // stream the checks of different jobs queue behind each other
+  const char* fev = getenv("BLS_FE_STREAM");
+  const bool fe_job = !(fev && !strcmp(fev, "ctx"));
   if (hipStreamCreateWithFlags(&c->fb_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->fe_stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      (!fe_job && hipStreamCreateWithPriority(&c->fe_stream, hipStreamNonBlocking, prio_hi) != hipSuccess)) {
     bls_ctx_destroy(c);
     return BLS_E_DEVICE;
   }
@@ -499,17 +528,20 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   if (msg_len) memcpy(ctx->pc_stage + 48 * n + 96, msg, msg_len);
   memcpy(ctx->pc_stage + offs_at, offs, sizeof offs);
   CK(h2d(ctx, d_in, ctx->pc_stage, total));
+  // a two-stream job 0 (stream3 aliases stream2): the signature check runs on stream1 ahead of the keys, beside
+  // the hash, instead of behind it
+  const hipStream_t ss = st3 == st2 ? st : st3;
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
-  HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
+  if (ss != st) HIPCK(hipStreamWaitEvent(ss, J.ev_fork, 0));
   // one wave of wavefront-cooperative arithmetic for the one message (bls_wide.h); 32-byte messages (every
   // signing root) take the register-resident expand_message_xmd
   const uint64_t* h_offs = msg_len == 32 ? nullptr : d_offs;
   LK(launch_h2c_wide(st2, 1, d_msg, h_offs, Q, flag));
   CK(h2c_fallback(ctx, st2, 1, d_msg, h_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
-  LK(launch_sig_validate_wide(st3, d_sig, 1, Q + 1, ok + n));
-  HIPCK(hipEventRecord(J.ev_sig, st3));
+  LK(launch_sig_validate_wide(ss, d_sig, 1, Q + 1, ok + n));
+  HIPCK(hipEventRecord(J.ev_sig, ss));
   LK(launch_keys(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
@@ -580,11 +612,12 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   CK(h2d(ctx, d_sig, sig96, 96));
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
+  const hipStream_t ss = st3 == st2 ? st : st3;  // two-stream job 0: the signature check on stream1 (verify_percall)
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
-  HIPCK(hipStreamWaitEvent(st3, J.ev_fork, 0));
-  LK(launch_sig_validate_wide(st3, d_sig, 1, Q + n, d_w));
-  HIPCK(hipEventRecord(J.ev_sig, st3));
+  if (ss != st) HIPCK(hipStreamWaitEvent(ss, J.ev_fork, 0));
+  LK(launch_sig_validate_wide(ss, d_sig, 1, Q + n, d_w));
+  HIPCK(hipEventRecord(J.ev_sig, ss));
   bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
   for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
   if (n <= WIDE_H2C_MAX)  // a few messages: one wave each, lower latency than the lane kernels' chains
@@ -600,7 +633,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   const int v = validate_pks(ctx, pks48, n, &P, &ok);  // synchronises stream1
   if (v <= 0) {
     HIPCK(hipStreamSynchronize(st2));  // the scratch of the side streams is reused by the next call
-    HIPCK(hipStreamSynchronize(st3));
+    HIPCK(hipStreamSynchronize(ss));
     return v;
   }
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
@@ -1007,96 +1040,99 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
     ctx->err = "no registry loaded";
     return BLS_E_NOREG;
   }
+  // pairs 0 .. B: (r_i apk_i, H_i); pairs B .. B + 64: (-2^b G1, U_b), the MSM's bit-sums (bls_msm.hip)
+  const size_t NP = B + MSM_UPAIRS;
   int *status, *gstat, *flag, *dstat;
   G1P *apka, *rpj;
   G1A* rP;
-  G2A *sig, *H, *saff;
+  G2A *sig, *H;
   Fp12 *f, *ft, *fo;
   Fd *msmf, *hcf;
   uint64_t* rsc;
   uint32_t* msmu;
   uint8_t* d_seed;
-  SCR(S_STATUS, B + 1, status);
+  SCR(S_STATUS, NP, status);
   SCR(S_GSTAT, B, gstat);
   SCR(S_APKA, B, apka);
   SCR(S_SIG, B, sig);
-  SCR(S_RP, B + 1, rP);
-  SCR(S_H, B, H);
+  SCR(S_RP, NP, rP);
+  SCR(S_H, NP, H);
   SCR(S_FLAG, B, flag);
   SCR(S_RSC, B, rsc);
   SCR(S_MSMU, msm_scratch_u32(B), msmu);
   SCR(S_MSMF, msm_scratch_fd(), msmf);
   SCR(S_HCF, h2c_scratch_fd(B), hcf);
   SCR(S_RPJ, B, rpj);
-  // Miller loop of (r_i apk_i, H_i), split: G2 lines (k_miller_lines2) on stream2 right after hash_to_G2, f
-  // accumulated on stream1 by k_miller_acc4<2> (four lanes per f, two pairs per f: one squaring per step for both)
+  // Miller loop of all NP pairs, split: G2 lines (k_miller_lines2) on stream2 after hash_to_G2 and the MSM, f
+  // accumulated on stream1 by k_miller_acc4q (four lanes per f, G pairs per f: one squaring per step for all G)
   uint32_t* mlines;
-  SCR(S_MLINES, miller_lines_u32(B), mlines);
-  SCR(S_SAFF, 1, saff);
+  SCR(S_MLINES, miller_lines_u32(NP), mlines);
   SCR(S_MSTAT, B, dstat);
-  SCR(S_FAV_F, B + 2, f);  // per-item (or per-group) f, kept for the bisection: not S_F, which per-call checks use
-  SCR(S_FAV_FT, (B + 1) / 8 + 16, ft);
+  SCR(S_FAV_F, NP, f);  // per-item (or per-group) f, kept for the bisection: not S_F, which per-call checks use
+  SCR(S_FAV_FT, NP / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
   SCR(S_SEED, 32, d_seed);
-  hipStream_t st = ctx->j->stream, st2 = ctx->j->stream2, st3 = ctx->j->stream3;
+  Job& J = *ctx->j;
+  hipStream_t st = J.stream, st2 = J.stream2, st3 = J.stream3;
+  if (!ctx->comb) {  // the -G1 comb (bls_bisect.hip): the MSM pairs' -2^b G1 and the bisection's -r_i G1
+    HIPCK(hipMalloc(&ctx->comb, neg_g1_comb_entries() * sizeof(G1A)));
+    LK(launch_neg_g1_comb_table(st, ctx->comb));
+    HIPCK(hipStreamSynchronize(st));
+  }
+  // a two-stream job (stream3 == stream2, BLS_JOB_STREAMS=2, the default): the decode and the MSM run on stream1
+  // around the gather, off the hash -> lines chain of stream2
+  const bool two = st3 == st2;
+  hipStream_t sd = two ? st : st3;
   // the branches fork from stream1's tail -- or, after a bisection still running there, from the point where it
-  // has copied everything it reads of the state stream2 / stream3 write (fav_bisect); the seed goes on stream3,
-  // its reader, so the fork need not follow stream1
-  HIPCK(hipMemcpyAsync(d_seed, seed32, 32, hipMemcpyHostToDevice, st3));
-  // Three branches:
-  //   stream1: registry gather (affine apk) -> subgroup / r_i apk_i chains -> Miller loops
-  //   stream2: hash_to_G2 of every message
-  //   stream3: signature decompression + RLC scalars -> MSM S = sum r_i sigma_i
-  //            -> Miller loop of (-G1, S) -> f[B + 1]
-  hipEvent_t fork = ctx->j->ev_fork;
-  if (ctx->j->bis_pending) {
-    fork = ctx->j->ev_bis;
-    ctx->j->bis_pending = false;
+  // has copied everything it reads of the state stream2 / stream3 write (fav_bisect); the seed goes on the
+  // decode's stream, its reader, so the fork need not follow stream1
+  HIPCK(hipMemcpyAsync(d_seed, seed32, 32, hipMemcpyHostToDevice, sd));
+  // Branches, three streams:
+  //   stream1: registry gather (affine apk) -> subgroup / r_i apk_i chains -> f accumulation
+  //   stream2: hash_to_G2 of every message -> (after the MSM) the G2 lines of all NP pairs
+  //   stream3: signature decompression + RLC scalars -> MSM bit-sums U_b of S = sum r_i sigma_i
+  // two streams: stream3's work on stream1 (decode before the gather, MSM after it)
+  hipEvent_t fork = J.ev_fork;
+  if (J.bis_pending) {
+    fork = J.ev_bis;
+    J.bis_pending = false;
   } else {
     HIPCK(hipEventRecord(fork, st));
   }
   HIPCK(hipStreamWaitEvent(st2, fork, 0));
-  HIPCK(hipStreamWaitEvent(st3, fork, 0));
+  if (!two) HIPCK(hipStreamWaitEvent(st3, fork, 0));
   PROF2(2, st2, launch_h2c(st2, B, d_msgs, nullptr, hcf, H, flag));
   CK(h2c_fallback(ctx, st2, B, d_msgs, nullptr, flag, H));
-  PROF2(12, st2, launch_miller_lines(st2, H, B, mlines));
-  HIPCK(hipEventRecord(ctx->j->ev_join, st2));
-  PROF2(1, st3, launch_sig_decode(st3, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
-  HIPCK(hipEventRecord(ctx->j->ev_sig, st3));
+  PROF2(1, sd, launch_sig_decode(sd, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
+  HIPCK(hipEventRecord(J.ev_sig, sd));
   PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, (uint32_t)ctx->reg_n, apka, gstat));
-  HIPCK(hipEventRecord(ctx->j->ev_gather, st));
+  HIPCK(hipEventRecord(J.ev_gather, st));
   // The MSM covers every decoded signature of a valid aggregate key, before
   // the subgroup checks: a decodable signature outside G2 stays in S, so the
   // batch check fails and fav_finish re-checks every item individually.  It
   // reads only gstat (gather) and dstat (decode), which no kernel writes
   // after ev_gather / ev_sig; the subgroup verdicts go to `status`, written on
-  // stream1 while the MSM runs.
-  HIPCK(hipStreamWaitEvent(st3, ctx->j->ev_gather, 0));
-  {
-    ProfScope ps_(ctx, 11, st3);
-    LK(launch_msm(st3, B, gstat, dstat, rsc, sig, msmu, msmf, saff));
-    hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st3, rP + B);
-    LK(hipGetLastError());
-    // the one pair (-G1, S) on the fused wide Miller kernel (bls_wide.hip k_miller_wide): the MSM-side chain is
-    // latency, one wave per step of the lane kernel was ~2.1 ms of it
-    LK(launch_miller_wide(st3, rP + B, saff, nullptr, nullptr, 1, f + B + 1));
-  }
-  HIPCK(hipEventRecord(ctx->j->ev_msm, st3));
-  HIPCK(hipStreamWaitEvent(st, ctx->j->ev_sig, 0));
+  // stream1 while (or after) the MSM runs.
+  hipStream_t sm = two ? st : st3;
+  if (!two) HIPCK(hipStreamWaitEvent(sm, J.ev_gather, 0));
+  PROF2(11, sm, launch_msm_upairs(sm, B, gstat, dstat, rsc, sig, msmu, msmf, ctx->comb, rP + B, H + B, status + B));
+  HIPCK(hipEventRecord(J.ev_msm, sm));
+  // the lines of every pair: the hashes' (stream2) and the MSM's (ev_msm)
+  HIPCK(hipStreamWaitEvent(st2, J.ev_msm, 0));
+  PROF2(12, st2, launch_miller_lines(st2, H, NP, mlines));
+  HIPCK(hipEventRecord(J.ev_join, st2));
+  if (!two) HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   PROF(10, launch_sig_vm(st, B, gstat, status, dstat, apka, sig, rsc, rpj, rP));
-  // Miller loops of (r_i apk_i, H_i), their product -> f[B], times f[B + 1]
-  HIPCK(hipStreamWaitEvent(st, ctx->j->ev_join, 0));
+  HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
   // two pairs share each f (one squaring per step for both) on full batches; below ACC_SHARED_MIN items the
   // launch under-fills the chip and the chain latency is what counts, so one pair per f (a step is a squaring
   // and ONE line: ~37 % shorter chains for ~24 % more products)
   const int mg = B >= ACC_SHARED_MIN ? 2 : 1;
-  ctx->j->fav_mg = mg;
-  PROF(5, launch_miller_acc4(st, rP, H, status, B, mlines, f, mg));
-  PROF(6, launch_fp12_prod_vm(st, f, (B + mg - 1) / mg, ft, f + B));
-  HIPCK(hipStreamWaitEvent(st, ctx->j->ev_msm, 0));
-  LK(launch_fp12_prod_vm(st, f + B, 2, ft, fo));
-  ctx->j->fav_B = B;
-  ctx->j->fav_ready = true;
+  J.fav_mg = mg;
+  PROF(5, launch_miller_acc4(st, rP, H, status, NP, mlines, NP, f, mg));
+  PROF(6, launch_fp12_prod_vm(st, f, (NP + mg - 1) / mg, ft, fo));
+  J.fav_B = B;
+  J.fav_ready = true;
   *out_f = fo;
   return 0;
 }
@@ -1108,8 +1144,8 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
 //             ACC_SHARED_MIN items) or k_miller_acc4q<1> over the batch's line
 //             records again (shared-f batches);
 //   f_sig,i = ML(-r_i G1, sigma_i): -r_i G1 from a fixed-base comb (8 mixed
-//             additions), sigma_i's line records by k_miller_lines2 (written over
-//             the H records, which are no longer needed), f by k_miller_acc4q<1>;
+//             additions), sigma_i's line records by k_miller_lines2, f by
+//             k_miller_acc4q<1>;
 // leaf_i = f_H,i f_sig,i, and a 16-ary product tree above the leaves.  A node's
 // check is FE(node) == 1: the product of e(r_i apk_i, H_i) e(-r_i G1, sigma_i)
 // over its items, the random linear combination of their checks.  The first
@@ -1160,20 +1196,16 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   if (J.fav_mg > 1) SCR(S_BSEL, B, fH);
   else fH = fb;
   hipStream_t st = J.stream;
-  if (!ctx->comb) {  // the -G1 comb, once per context
-    HIPCK(hipMalloc(&ctx->comb, neg_g1_comb_entries() * sizeof(G1A)));
-    LK(launch_neg_g1_comb_table(st, ctx->comb));
-  }
   // first everything read of the state that the job's next batch writes from stream2 / stream3 (H and the line
   // records, sigma_i, r_i); that batch forks from ev_bis (fav_prepare) while the rest runs here
-  if (J.fav_mg > 1) LK(launch_miller_acc4(st, rP, H, status, B, mlines, fH, 1));
+  if (J.fav_mg > 1) LK(launch_miller_acc4(st, rP, H, status, B, mlines, B + MSM_UPAIRS, fH, 1));
   HIPCK(hipMemcpyAsync(sig, sig0, B * sizeof(G2A), hipMemcpyDeviceToDevice, st));
   HIPCK(hipMemcpyAsync(rsc, rsc0, B * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   HIPCK(hipEventRecord(J.ev_bis, st));
   J.bis_pending = true;
   LK(launch_neg_rg1(st, B, status, rsc, ctx->comb, Pj, Ps));
   LK(launch_miller_lines(st, sig, B, slines));
-  LK(launch_miller_acc4(st, Ps, sig, status, B, slines, fS, 1));
+  LK(launch_miller_acc4(st, Ps, sig, status, B, slines, B, fS, 1));
   LK(launch_fp12_chunk_prod2(st, fH, fS, B, 1, tree));
   for (int L = 0; L < top; L++) LK(launch_fp12_chunk_prod(st, tree + off[L], cnt[L], 16, tree + off[L + 1]));
   HIPCK(hipMemsetAsync(nchk, 0, sizeof(uint32_t), st));
@@ -1393,7 +1425,7 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
     uint32_t* mlines;
     SCR(S_AV_ML, miller_lines_u32(npair), mlines);
     LK(launch_miller_lines(st, Q2, npair, mlines));
-    PROF(5, launch_miller_acc4(st, P2, Q2, nullptr, npair, mlines, f, 1));
+    PROF(5, launch_miller_acc4(st, P2, Q2, nullptr, npair, mlines, npair, f, 1));
   } else {
     PROF(5, launch_miller_wave(st, P2, Q2, nullptr, npair, f));
   }
@@ -1782,8 +1814,39 @@ static int job_submit(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_off
   HIPCK(hipMemcpyAsync(J.h_partial, d_b, 576, hipMemcpyDeviceToHost, J.stream));
   HIPCK(hipEventRecord(J.ev_partial, J.stream));
   J.partial_pending = true;
-  J.own_check_failed = false;
+  // this job's own check, right behind its product on its stream: a single-GPU caller reads it with
+  // bls_fav_job_check_own (no host round trip of the partial), and a multi-GPU failure is localised by it
+  int* d_own;
+  SCR(S_OWN, 1, d_own);
+  PROF(7, launch_final_check_wave(J.stream, f, 1, d_own));
+  HIPCK(hipMemcpyAsync(J.h_own, d_own, sizeof(int), hipMemcpyDeviceToHost, J.stream));
+  HIPCK(hipEventRecord(J.ev_own, J.stream));
+  J.own_pending = true;
+  J.own_state = -1;
   return 1;
+}
+
+// *state = the job's own verdict (1 / 0; waits for the check job_submit enqueued).  Returns 0 or BLS_E_*.
+static int read_own(bls_ctx* ctx, int* state) {
+  Job& J = *ctx->j;
+  if (J.own_pending) {
+    HIPCK(hipEventSynchronize(J.ev_own));
+    J.own_state = J.h_own[0] ? 1 : 0;
+    J.own_pending = false;
+  }
+  if (J.own_state < 0) {
+    ctx->err = "no submitted FAV batch on this job";
+    return BLS_E_ARG;
+  }
+  *state = J.own_state;
+  return 0;
+}
+
+static int job_check_own(bls_ctx* ctx) {
+  int own = 0;
+  CK(read_own(ctx, &own));
+  ctx->j->partial_pending = false;  // the partial's host copy is not needed
+  return own;
 }
 
 static int job_partial(bls_ctx* ctx, uint8_t* partial576) {
@@ -1807,18 +1870,21 @@ static int job_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
   SCR(S_FCHK, n, f);
   CK(h2d(ctx, d_b, partials576, 576 * n));
   PROF(9, launch_fp12_from_bytes(ctx->j->stream, d_b, n, f));
-  const int r = run_final_check(ctx, f, (int)n);  // the n partials are multiplied inside the FE kernel
-  // one partial equal to this job's own: a failure localises to this job (its bisection skips the root check)
-  ctx->j->own_check_failed = r == 0 && n == 1 && ctx->j->h_partial && !memcmp(partials576, ctx->j->h_partial, 576);
-  return r;
+  return run_final_check(ctx, f, (int)n);  // the n partials are multiplied inside the FE kernel
 }
 
 // Verdicts are written on the job's stream: a failing batch's bisection runs there without a host round trip, so
 // the caller can check the next job meanwhile (bls_sync / bls_d2h wait for every job stream).
 static int job_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
   if (!d_out) return BLS_E_ARG;
-  CK(fav_finish(ctx, batch_ok, ctx->j->own_check_failed, d_out));
-  ctx->j->own_check_failed = false;
+  bool root_bad = false;
+  if (!batch_ok) {  // a failed product of several shards (or of given partials): this job's own check decides
+    int own = 0;
+    CK(read_own(ctx, &own));
+    if (own == 1) batch_ok = 1;  // its own product passes: the failure is elsewhere, every status stands
+    else root_bad = true;        // its own product fails: bisect below the root
+  }
+  CK(fav_finish(ctx, batch_ok, root_bad, d_out));
   return 1;
 }
 
@@ -1856,6 +1922,11 @@ int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576) {
 int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t n) {
   JOB_ENTER(ctx, job);
   return job_check(ctx, partials576, n);
+}
+
+int bls_fav_job_check_own(bls_ctx* ctx, int job) {
+  JOB_ENTER(ctx, job);
+  return job_check_own(ctx);
 }
 
 int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out) {
@@ -1954,9 +2025,7 @@ static int job_check_comm(bls_ctx* ctx) {
   if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllGather");
   J.partial_pending = false;  // consumed on the device (the pinned host copy is not waited for)
   PROF(9, launch_fp12_from_bytes(J.stream, d_all, W, f));
-  const int ok = run_final_check(ctx, f, W);
-  J.own_check_failed = ok == 0 && W == 1;
-  return ok;
+  return run_final_check(ctx, f, W);
 }
 
 int bls_fav_job_check_comm(bls_ctx* ctx, int job) {

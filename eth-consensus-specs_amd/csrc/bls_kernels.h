@@ -57,7 +57,11 @@ hipError_t launch_sig_vm(hipStream_t st, size_t B, const int* gstat, int* status
                          const G2A* sig, const uint64_t* rsc, G1P* rPj, G1A* rP);
 size_t msm_scratch_u32(size_t B);
 size_t msm_scratch_fd();
-hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc, const G2A* sig, uint32_t* scr, Fd* pts, G2A* out);
+// the 64 bit-sums U_b of S = sum_i r_i sigma_i = sum_b 2^b U_b as Miller pairs (-2^b G1, U_b) at P[0 .. 64),
+// Q[0 .. 64), ok[0 .. 64) = 1; comb: the bisection's -G1 comb (neg_g1_comb_entries() entries)
+constexpr int MSM_UPAIRS = 64;
+hipError_t launch_msm_upairs(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc,
+                             const G2A* sig, uint32_t* scr, Fd* pts, const G1A* comb, G1A* P, G2A* Q, int* ok);
 // the same Miller values in two kernels (G2 lines, then f); L: miller_lines_u32(n) words of scratch
 constexpr int MILLER_NLINES = 68;  // 63 doublings + 5 additions (|x| = 0xd201000000010000)
 // Miller line records (k_miller_lines2 -> k_miller_acc4q): three Fp2 -- (l0, E ZZ, z3 ZZ) for a doubling, (l0, r,
@@ -67,9 +71,10 @@ constexpr int ML_WORDS = 84;
 constexpr uint64_t ML_LV = 4096, ML_LD = 0x20000000ull + 64;
 size_t miller_lines_u32(size_t n);
 hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L);
-// four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values
+// four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values; ld >= n: the
+// line records' leading dimension (the n of the launch_miller_lines that wrote them)
 hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
-                              Fp12* f, int G);
+                              size_t ld, Fp12* f, int G);
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out);
 // one bisection-tree level: node b is checked (res[b] = FE(node[b]) == 1, ++*nchecks) when parent is null or
 // parent[b / pdiv] == 0, else res[b] = 1 (bls_fe.hip k_fe_check_gated)
@@ -112,8 +117,6 @@ hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const 
 hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out);
 // signature decode + subgroup check with one wave per signature (k_sig_validate semantics)
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
-// S = sum_b 2^b U_b of the MSM's 64 bit-sums (packed projective, bls_msm.hip) on one 16-wave workgroup
-hipError_t launch_msm_weighted_wide(hipStream_t st, const Fp* U, G2A* out);
 // the whole Miller loop of npairs <= 2 pairs on one workgroup (line waves + six f waves): out = f (tower Fp12);
 // ok0 / ok1 (nullable): pair 0 / 1 runs with constant lines unless *okp
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,

@@ -184,9 +184,11 @@ __device__ __forceinline__ void qq_line_p(const LineIn& in, const FqB<VP, DP>& p
 
 }  // namespace
 
+// n pairs; their line records with leading dimension ld >= n (word w of line k of pair i at L[(k ML_WORDS + w) ld
+// + i]: the bisection re-reads the first B records of a batch written for B + 64 pairs)
 template <int G>
 __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q, const int* ok, size_t n,
-                                                     const uint32_t* L, Fp12* out) {
+                                                     const uint32_t* L, size_t ld, Fp12* out) {
   const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
   const size_t grp = t >> 2;
   const bool h = (t & 2) != 0, q = (t & 1) != 0;
@@ -211,7 +213,7 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
   }
   constexpr uint64_t VF = ML_QF_V, DF = ML_QF_D;
   using F = Fq6B<VF, DF>;
-  const size_t step = (size_t)ML_WORDS * n;
+  const size_t step = (size_t)ML_WORDS * ld;
   const uint32_t* Lb[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) Lb[g] = L + pi[g];
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
     for (int s = 0; s < nl; ++s) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const LineIn cur = ld_line(Lb[g], n, h, q);
+        const LineIn cur = ld_line(Lb[g], ld, h, q);
         Fq2B<2, fqb_detail::MASK> l2, l3;
         qq_line_p(cur, sel(g == 0, pc0, pc1), q, l2, l3);
         const auto fl = relax<VF, DF>(qq_line(f, h, q, cur.l0, l2, l3));
@@ -249,14 +251,15 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
 }
 
 hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
-                              Fp12* f, int G) {
+                              size_t ld, Fp12* f, int G) {
   if (!n) return hipSuccess;
+  if (ld < n) return hipErrorInvalidValue;
   const size_t ngrp = (n + G - 1) / G;
   const dim3 grid((unsigned)((4 * ngrp + 63) / 64));
   if (G == 2)
-    hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
+    hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   else
-    hipLaunchKernelGGL(k_miller_acc4q<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, f);
+    hipLaunchKernelGGL(k_miller_acc4q<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   return hipGetLastError();
 }
 

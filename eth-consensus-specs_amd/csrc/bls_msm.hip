@@ -12,15 +12,21 @@
 //                   wave per b, 32 lane pairs adding 4 bucket sums each, then a
 //                   5-level LDS tree (a 16-wave wide-arithmetic variant
 //                   measured C2 -4 %: profiles/r04o_usum_ab.txt)
-//   k_msm_weighted_wide  S = sum_b 2^b U_b in wavefront-cooperative arithmetic,
-//                   one 16-wave workgroup (bls_msm_wide.hip; the lane-pair tree
-//                   it replaces took ~1.6 ms of latency per batch), S -> affine
-// ~8 additions per signature instead of a 64-step double-and-add; the chain
-// runs on its own high-priority stream beside the Miller loops of the
-// (r_i apk_i, H_i) pairs.  (The previous form ran one lane pair per bucket --
-// 64 waves, ~40 dependent additions with unprefetched loads -- and 13 tree
-// launches: ~6.8 ms per C2 batch.)
+//   k_msm_upairs    the 64 pairs (-2^b G1, U_b), U_b affine: the Miller loop
+//                   of (-G1, S) with S = sum_b 2^b U_b is, after the final
+//                   exponentiation, the product of e(-2^b G1, U_b) -- so the
+//                   U_b join the batch's own pairs (lines + f accumulation)
+//                   and the 63-doubling weighted sum S (round 4:
+//                   k_msm_weighted_wide, one 16-wave workgroup, ~0.7 ms) and
+//                   its one-pair Miller loop (k_miller_wide, ~0.5 ms) leave
+//                   the latency chain.  The -2^b G1 are entries of the
+//                   bisection's fixed-base comb (bls_bisect.hip).
+// ~8 additions per signature instead of a 64-step double-and-add.  (The
+// previous form ran one lane pair per bucket -- 64 waves, ~40 dependent
+// additions with unprefetched loads -- and 13 tree launches: ~6.8 ms per C2
+// batch.)
 #include "bls_kernels.h"
+#include "bls_fp_inv.h"
 #include "bls_pp_lane.h"
 
 
@@ -162,13 +168,30 @@ __global__ void __launch_bounds__(64) k_msm_usum(const Fp* csum, Fp* U) {
   if (j == 0) p2_store(U + 6 * b, R, hi);
 }
 
+// lane b < 64: pair (-2^b G1, U_b) at P[b], Q[b], ok[b] = 1 (U_b = the identity: Q[b].inf, a skipped pair).
+// -2^b G1 = comb[256 (b / 8) + 2^(b % 8)] (comb[256 w + d] = d 2^(8 w) (-G1)).
+__global__ void __launch_bounds__(64) k_msm_upairs(const Fp* U, const G1A* comb, G1A* P, G2A* Q, int* ok) {
+  const int b = threadIdx.x;
+  const Fp* u = U + 6 * b;
+  const Fp2 X{u[0], u[1]}, Y{u[2], u[3]}, Z{u[4], u[5]};
+  G2A q{fp2_zero(), fp2_zero(), true};
+  if (!fp2_is_zero(Z)) {  // homogeneous projective (RCB): x = X / Z, y = Y / Z
+    const Fp ni = fp_inv_sg_i(fp_add(fp_sqr_i(Z.c0), fp_sqr_i(Z.c1)));  // 1 / norm(Z)
+    const Fp2 zi{fp_mul_i(Z.c0, ni), fp_neg(fp_mul_i(Z.c1, ni))};
+    q = G2A{f2mul(X, zi), f2mul(Y, zi), false};
+  }
+  Q[b] = q;
+  P[b] = comb[256 * (b >> 3) + (1 << (b & 7))];
+  ok[b] = 1;
+}
+
 // Scratch: cnt[MSM_NB] | off[MSM_NB + 1] | cur[MSM_NB] (u32), lst[8 B] (u32);
 // points (packed Fp, 6 per point, in units of Fd slots): chunk sums [MSM_NB * MSM_C] | U [64].
 size_t msm_scratch_u32(size_t B) { return (size_t)3 * MSM_NB + 1 + MSM_W * B; }
 size_t msm_scratch_fd() { return ((size_t)(MSM_NB * MSM_C + 64) * 6 * sizeof(Fp) + sizeof(Fd) - 1) / sizeof(Fd); }
 
-hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc,
-                      const G2A* sig, uint32_t* scr, Fd* pts, G2A* out) {
+hipError_t launch_msm_upairs(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc,
+                             const G2A* sig, uint32_t* scr, Fd* pts, const G1A* comb, G1A* P, G2A* Q, int* ok) {
   uint32_t* cnt = scr;
   uint32_t* off = cnt + MSM_NB;
   uint32_t* cur = off + MSM_NB + 1;
@@ -192,7 +215,8 @@ hipError_t launch_msm(hipStream_t st, size_t B, const int* status, const int* st
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_usum, dim3(64), dim3(2 * USUM_PAIRS), 0, st, csum, U);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_msm_weighted_wide(st, U, out);
+  hipLaunchKernelGGL(k_msm_upairs, dim3(1), dim3(64), 0, st, U, comb, P, Q, ok);
+  return hipGetLastError();
 }
 
 }  // namespace bls

@@ -37,8 +37,9 @@ extern "C" {
 
 typedef struct bls_ctx bls_ctx;
 
-/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 7) get streams. */
-#define BLS_FAV_JOBS 8
+/* FAV batch slots of one context (bls_fav_job_*): the first BLS_FAV_JOBS_INIT (env, default 10) get streams
+ * (BLS_JOB_STREAMS per job, default 2). */
+#define BLS_FAV_JOBS 16
 
 /* Context on HIP device `device` (ordinal).  Returns 0 or BLS_E_*. */
 int bls_ctx_create(int device, bls_ctx** out);
@@ -233,8 +234,7 @@ int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out);
  * / bls_fav_batch_finish_dev (those are job 0, submitted and waited at once).
  *   submit:  enqueue the batch, return at once (1 or BLS_E_*)
  *   partial: wait for the job's 576-byte Miller product
- *   check:   final exponentiation of the product of n partials on the job's
- *            stream: 1 / 0
+ *   check:   final exponentiation of the product of n partials: 1 / 0
  *   finish:  verdicts into d_out, enqueued on the job's stream without a host
  *            wait -- a failing batch's bisection runs there on the device (no
  *            host round trip per round) while the host checks the next job;
@@ -243,6 +243,12 @@ int bls_fav_job_submit_dev(bls_ctx* ctx, int job, const uint32_t* d_idx, const u
                            const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32);
 int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576);
 int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t n);
+/* check_own: the final exponentiation of the job's own product alone, which
+ * submit already enqueued on the job's stream (the single-GPU check: no host
+ * round trip of the partial): 1 / 0.  A finish after a failed multi-shard
+ * check uses the same verdict -- a job whose own product passes keeps every
+ * per-item status, one whose own product fails bisects below its root. */
+int bls_fav_job_check_own(bls_ctx* ctx, int job);
 int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out);
 
 /* ---- multi-GPU exchange over RCCL ----------------------

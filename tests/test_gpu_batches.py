@@ -298,8 +298,8 @@ def test_resident_batch_chunked(batch, registry):
 @pytest.mark.parametrize("B", [1, 2, 5])
 def test_fav_small_batch_msm_identities(batch, registry, B):
     """Batches of 1, 2 and 5 items: most of the MSM's 64 bit-sums U_b are the identity (only the bits the few RLC
-    scalars set), so the wide weighted sum (k_msm_weighted_wide, complete projective formulas) must carry
-    identities through doublings and additions; a wrong S would fail the batch check and show as fallback work."""
+    scalars set), so most of the 64 pairs (-2^b G1, U_b) the MSM adds to the batch's Miller loops (k_msm_upairs)
+    are skipped identities; a wrong or mis-skipped pair would fail the batch check and show as fallback work."""
     idx, offs, msgs, sigs = _make_batch(batch, B, 8, seed=40 + B)
     out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
     assert out.all()

@@ -6,9 +6,8 @@ CPU run.
 
   k_fe_wide (bls_fe_wide.hip): Fp12 product per w-coefficient, Granger-Scott cyclotomic squaring with the
       +-2 terms as products, Frobenius maps with the per-coefficient gamma tables, the hard-part schedule.
-  k_miller_wide / k_facc_wide (bls_wide.hip): f^2 through the FSQ_TERMS table, f * sparse line (l0, l2, l3).
-  k_msm_weighted_wide (bls_msm_wide.hip): complete projective addition / doubling with the cross terms as
-      sums of products (t3 = X1 Y2 + Y1 X2, ...) and 3b = 12 xi.
+  k_miller_wide (bls_wide.hip): f^2 through the FSQ_TERMS table, f * sparse line (l0, l2, l3).
+  k_msm_upairs (bls_msm.hip): the MSM's 64 bit-sums as Miller pairs (-2^b G1, U_b) in place of the weighted sum.
 """
 import os
 import random
@@ -171,78 +170,22 @@ def test_miller_wide_square_and_line():
         assert fl == O.f12_to_coeffs(O.f12_mul(fa, line))
 
 
-# ---- k_msm_weighted_wide complete projective formulas --------------------------------------------------------
-def b3(t):
-    return muls(xi(t), 12)
-
-
-def p2f_dbl(p):
-    X, Y, Z = p
-    t0, t1, t2, u = mul(Y, Y), mul(Y, Z), b3(mul(Z, Z)), mul(X, Y)
-    z8 = muls(t0, 8)
-    w = sub(t0, muls(t2, 3))
-    return (mul(w, muls(u, 2)), add(mul(w, add(t0, t2)), mul(t2, z8)), mul(t1, z8))
-
-
-def p2f_add(p, q):
-    X1, Y1, Z1 = p
-    X2, Y2, Z2 = q
-    t0, t1, t2 = mul(X1, X2), mul(Y1, Y2), mul(Z1, Z2)
-    t3 = add(mul(X1, Y2), mul(Y1, X2))
-    t4 = add(mul(Y1, Z2), mul(Z1, Y2))
-    y3 = b3(add(mul(X1, Z2), mul(Z1, X2)))
-    bt2 = b3(t2)
-    t0x3 = muls(t0, 3)
-    z3 = add(t1, bt2)
-    t1m = sub(t1, bt2)
-    return (add(mul(t3, t1m), mul(y3, O.f2_neg(t4))), add(mul(t1m, z3), mul(y3, t0x3)), add(mul(z3, t4), mul(t0x3, t3)))
-
-
-def to_aff(p):
-    X, Y, Z = p
-    if Z == O.F2_ZERO:
-        return None
-    zi = O.f2_inv(Z)
-    return (mul(X, zi), mul(Y, zi))
-
-
-def proj(pt, r):
-    if pt is None:
-        return (O.F2_ZERO, O.F2_ONE, O.F2_ZERO)
-    z = rnd_f2(r)
-    return (mul(pt[0], z), mul(pt[1], z), z)
-
-
-def test_msm_wide_complete_formulas():
-    r = random.Random(0xFE04)
-    g = O.G2_GEN if hasattr(O, "G2_GEN") else O.hash_to_g2(b"wide formulas")
-    pts = [O.g2_mul(g, r.randrange(1, O.R)) for _ in range(3)]
-    a, b = pts[0], pts[1]
-    cases = [(a, b), (a, a), (a, O.g2_neg(a)), (a, None), (None, b), (None, None)]
-    for p, q in cases:
-        assert to_aff(p2f_add(proj(p, r), proj(q, r))) == O.g2_add(p, q)
-    for p in (a, None):
-        assert to_aff(p2f_dbl(proj(p, r))) == O.g2_add(p, p)
-    # the weighted sum's Horner + tree shape: sum_b 2^b U_b for U_b in {points, identity}
-    U = [pts[r.randrange(3)] if r.random() < 0.7 else None for _ in range(64)]
-    T = []
-    for j in range(16):
-        t = proj(U[j + 48], r)
-        for i in (32, 16, 0):
-            for _ in range(16):
-                t = p2f_dbl(t)
-            t = p2f_add(t, proj(U[j + i], r))
-        T.append(t)
-    s = 8
-    while s >= 1:
-        for j in range(s):
-            bp = T[j + s]
-            for _ in range(s):
-                bp = p2f_dbl(bp)
-            T[j] = p2f_add(T[j], bp)
-        s >>= 1
-    want = None
-    for bit in range(64):
-        if U[bit] is not None:
-            want = O.g2_add(want, O.g2_mul(U[bit], 1 << bit))
-    assert to_aff(T[0]) == want
+# ---- the MSM's bit-sum pairs (bls_msm.hip k_msm_upairs) ------------------------------------------------------
+def test_msm_bit_sum_pairs_replace_the_weighted_sum():
+    """fav_prepare no longer forms S = sum_b 2^b U_b: the 64 pairs (-2^b G1, U_b) join the batch's Miller loops,
+    since prod_b e(-2^b G1, U_b) = e(-G1, sum_b 2^b U_b).  The -2^b G1 are comb entries 256 (b / 8) + 2^(b % 8)
+    of the bisection's fixed-base table comb[256 w + d] = d 2^(8 w) (-G1) (bls_bisect.hip).  Checked here on a
+    few nonzero bit-sums (identity U_b are skipped pairs) with the oracle's pairing."""
+    g = O.hash_to_g2(b"msm bit sums")
+    bits = {0: 5, 9: 11, 40: 3, 63: 7}  # b -> U_b = k G
+    neg_g1 = O.g1_neg(O.G1_GEN)
+    f = O.F12_ONE
+    S = None
+    for b, k in bits.items():
+        comb_index = 256 * (b // 8) + (1 << (b % 8))
+        w, d = divmod(comb_index, 256)
+        assert d * (1 << (8 * w)) == 1 << b
+        f = O.f12_mul(f, O.miller_loop(O.g1_mul(neg_g1, d << (8 * w)), O.g2_mul(g, k)))
+        S = O.g2_add(S, O.g2_mul(g, k << b))
+    f = O.f12_mul(f, O.miller_loop(O.G1_GEN, S))  # times e(G1, S): the product is 1 iff the decomposition holds
+    assert O.final_exponentiation(f) == O.F12_ONE

@@ -38,6 +38,16 @@ for s in $STEPS; do
         "profiles/${TAG}_kernel_stats.md (rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu)" > /dev/null; fi
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
       tail -2 "$OUT/prof.log" ;;
+    profc2)
+      # C2 only, one batch at a time (--no-pipeline): the per-(kernel, grid) averages bench.py's frac_rocprof reads
+      # (profiles/rocprof_kernel_avg.json), comparable with its one-batch-at-a-time hipEvent figure
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/profc2" -o run -- \
+        python3 bench.py --no-cpu --no-pipeline --steps 20 --c3-steps 0 --c4-steps 0 --c5-steps 0 --no-percall \
+        --no-parity --no-e2e > "$OUT/profc2.log" 2>&1 || { tail -30 "$OUT/profc2.log"; exit 1; }
+      db=$(find "$OUT/profc2" -name '*.db' | head -n 1)
+      if [ -n "$db" ]; then python3 tools/rocprof_summary.py "$db" "$OUT/c2_kernel_stats.md" "$OUT/rocprof_kernel_avg.json" \
+        "profiles/${TAG}_c2_kernel_stats.md (rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu --no-pipeline --steps 20 --c3-steps 0 --c4-steps 0 --c5-steps 0 --no-percall --no-parity --no-e2e)" > /dev/null; fi
+      tail -1 "$OUT/profc2.log" | cut -c1-300 ;;
     percall)
       timeout -k 10 120 python3 tools/percall_probe.py > "$OUT/percall.json" 2> "$OUT/percall.err" \
         || { tail -20 "$OUT/percall.err"; exit 1; }

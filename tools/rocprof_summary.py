@@ -40,10 +40,17 @@ def main(db, out=None, out_json=None, source=None):
     if out:
         open(out, "w").write(text)
     if out_json:
-        avg = {r[0].split("(")[0].replace("void ", "").replace("bls::", ""): round(r[3] / 1e6, 4) for r in rows}
+        sym = lambda n: n.split("(")[0].replace("void ", "").replace("bls::", "")  # noqa: E731
+        avg = {sym(r[0]): round(r[3] / 1e6, 4) for r in rows}
+        # per (kernel, grid): one kernel launched at several sizes (e.g. k_miller_acc4q<2> for C2's 10,000 pairs
+        # and C4's 125,000) has one average per launch size; bench.py reads the entry of its own launch
+        by_grid: dict = {}
+        for name, grid, n, a in c.execute("select name, grid_x, count(*), avg(duration) from kernels "
+                                          "group by name, grid_x"):
+            by_grid.setdefault(sym(name), {})[str(grid)] = {"calls": n, "avg_ms": round(a / 1e6, 4)}
         with open(out_json, "w") as fh:
-            json.dump({"source": source or out or db, "avg_ms": avg, "lib_sha256_16": _lib_sha()}, fh, indent=1,
-                      sort_keys=True)
+            json.dump({"source": source or out or db, "avg_ms": avg, "avg_ms_by_grid": by_grid,
+                       "lib_sha256_16": _lib_sha()}, fh, indent=1, sort_keys=True)
     print(text)
 
 
