@@ -494,9 +494,11 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--c4-total", type=int, default=C4_TOTAL)
     ap.add_argument("--c5-bad", type=int, default=8, help="C5: bad items per batch (kinds cycled)")
-    ap.add_argument("--c3-steps", type=int, default=20, help="epochs timed for the c2 line's C3 figure (0: skip)")
+    # the secondary figures time enough passes to fill the 10-job pipeline several times over (5 C5 passes with 10
+    # jobs in flight measured mostly the fill and drain: 288k against 578k FAV/s at 30)
+    ap.add_argument("--c3-steps", type=int, default=60, help="epochs timed for the c2 line's C3 figure (0: skip)")
     ap.add_argument("--c4-steps", type=int, default=4, help="125k-Verify shards timed for the c2 line's C4 figure")
-    ap.add_argument("--c5-steps", type=int, default=5, help="adversarial batches timed for the c2 line's C5 figure")
+    ap.add_argument("--c5-steps", type=int, default=40, help="adversarial batches timed for the c2 line's C5 figure")
     ap.add_argument("--no-regload", action="store_true", help="generate the registry instead of loading its keys")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -549,8 +551,13 @@ def main():
         return float(t.item())
 
     def timed(rb, steps, warmup, depth=None):
-        """warmup + `steps` timed passes of rb between barriers; max over ranks; every pass must pass."""
+        """warmup + `steps` timed passes of rb between barriers; max over ranks; every pass must pass.  Setup
+        first: one pass on every job slot, so each slot's device scratch is allocated (hipMalloc) before the
+        timed region (a slot allocates on its first batch; with 10 slots and 2 warmup passes, 8 allocations
+        would land inside it)."""
         d = 1 if args.no_pipeline else (batch.FAV_DEPTH if depth is None else depth)
+        prime = -(-batch.FAV_JOBS // rb.chunks) if d > 1 else 1  # passes covering every slot (a pass = `chunks` jobs)
+        rb.run_pipelined([os.urandom(32) for _ in range(prime)], depth=d, comm=comm)
         if warmup:
             rb.run_pipelined([os.urandom(32) for _ in range(warmup)], depth=d, comm=comm)
         barrier_sync()

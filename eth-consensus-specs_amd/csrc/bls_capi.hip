@@ -1209,17 +1209,21 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   LK(launch_fp12_chunk_prod2(st, fH, fS, B, 1, tree));
   for (int L = 0; L < top; L++) LK(launch_fp12_chunk_prod(st, tree + off[L], cnt[L], 16, tree + off[L + 1]));
   HIPCK(hipMemsetAsync(nchk, 0, sizeof(uint32_t), st));
+  // the gated levels on the one-wave k_fe_check (chip time: with ten jobs in flight, C5 578k vs 519k FAV/s on the
+  // six-wave k_fe_wide, profiles/r05k_c5_bisect_fe_ab.txt) or, BLS_BISECT_FE=wide, on k_fe_wide (latency)
+  static const bool wide_fe = getenv("BLS_BISECT_FE") && !strcmp(getenv("BLS_BISECT_FE"), "wide");
+  auto gated = wide_fe ? launch_fe_wide_gated : launch_final_check_gated;
   uint64_t rounds = 0;
   const int* parent = nullptr;
   uint32_t pdiv = 1;
   if (!root_bad && T < R) {  // the root first; level T then runs only if it failed
-    LK(launch_fe_wide_gated(st, tree + off[R], 1, nullptr, 1, res + off[R], nchk));
+    LK(gated(st, tree + off[R], 1, nullptr, 1, res + off[R], nchk));
     parent = res + off[R];
     pdiv = (uint32_t)cnt[T];
     rounds++;
   }
   for (int L = T; L >= 0; L--) {
-    LK(launch_fe_wide_gated(st, tree + off[L], cnt[L], parent, pdiv, res + off[L], nchk));
+    LK(gated(st, tree + off[L], cnt[L], parent, pdiv, res + off[L], nchk));
     parent = res + off[L];
     pdiv = 16;
     rounds++;
