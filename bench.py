@@ -73,13 +73,18 @@ FME_OPS = 288  # one 381-bit Montgomery multiplication = 288 v_mad_u64_u32 (SURV
 SHA_OPS = 2400  # one SHA-256 compression
 MEASURED_MAD_OPS = 31.3e12  # sustained v_mad_u64_u32 lane-ops/s, profiles/r01_s2_madrate_microbench.txt
 SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
+# a FAV batch's Miller loops run split (k_miller_lines2 + k_miller_acc4q) unless BLS_MILLER_FUSED=1 selects the
+# fused kernel (k_miller_fused: G2 lines and f accumulation in one workgroup, lines in LDS; bls_capi.hip)
+MILLER_FUSED = os.environ.get("BLS_MILLER_FUSED") == "1"
+MSM_PAIRS = 64  # the MSM's bit-sum pairs (-2^b G1, U_b) join every batch's Miller loops (bls_msm.hip)
 # lanes per item of the lane kernels (full register file, one wave per SIMD): k_miller_acc4<2> four lanes per two
 # pairs (bls_miller_pair.hip), k_miller_lines2 two per pair (bls_miller_lane.hip), k_sig_lane2 one for the G1
 # chain and two for the G2 chain of an item (bls_chain_lane.hip)
-LANE_KERNELS = {"miller": 2, "miller_lines": 2, "sig_vm": 3}
+LANE_KERNELS = {"miller": 3 if MILLER_FUSED else 2, "miller_lines": 2, "sig_vm": 3}
 GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
 # profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
-KERNEL_SYMBOL = {"miller": "k_miller_acc4q<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
+KERNEL_SYMBOL = {"miller": "k_miller_fused<2>" if MILLER_FUSED else "k_miller_acc4q<2>", "miller_lines": "k_miller_lines2",
+                 "fav_gather": "k_fav_gather_q<16>"}
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 LIB = os.path.join(ROOT, "eth-consensus-specs_amd", "libblsmi355x.so")
 
@@ -93,10 +98,14 @@ C4_TOTAL, C4_CHUNK = 10 ** 6, 125_000
 
 
 def launch_grid(kernel: str, items: int) -> int | None:
-    """Threads of one launch of the roofline kernel over `items` FAV items (rocprofv3's grid_x): k_miller_acc4q<2>
-    runs 4 lanes per two pairs, k_miller_lines2 2 lanes per pair, k_fav_gather_q<16> 16 lanes per aggregate;
-    64-lane workgroups (bls_miller_pair.hip, bls_miller_lane.hip, bls_kernels.hip)."""
-    lanes = {"miller": 4 * ((items + 1) // 2), "miller_lines": 2 * items, "fav_gather": 16 * items}.get(kernel)
+    """Threads of one launch of the roofline kernel over `items` FAV items (rocprofv3's grid_x).  The Miller
+    kernels run items + 64 pairs (the MSM's bit-sum pairs): k_miller_fused<2> one 192-thread workgroup per 64 pairs,
+    k_miller_acc4q<2> 4 lanes per two pairs in 64-lane workgroups, k_miller_lines2 2 lanes per pair;
+    k_fav_gather_q<16> 16 lanes per aggregate (bls_miller_pair.hip, bls_miller_lane.hip, bls_kernels.hip)."""
+    np_ = items + MSM_PAIRS
+    if kernel == "miller" and MILLER_FUSED:
+        return (np_ + 63) // 64 * 192
+    lanes = {"miller": 4 * ((np_ + 1) // 2), "miller_lines": 2 * np_, "fav_gather": 16 * items}.get(kernel)
     return None if lanes is None else (lanes + 63) // 64 * 64
 
 
@@ -107,10 +116,11 @@ def model_fme(n: int):
         "sig_decode": 1200,             # signature decompression (Fp2 square root)
         "sig_vm": 1200 + 1000 + 400,    # G2 subgroup check, RLC G1, RLC G2 (MSM share)
         "fav_hash": 6600,
-        # Miller loop, 4400 FME per pair, split between its two kernels in proportion to the products each
-        # executes per pair: k_miller_acc4<2> (f shared by two pairs: 62 Fp12 squarings x 36 / 2 + 68 sparse
-        # line products x 43 = 4040) and k_miller_lines2 (T: 63 doublings x 26 + 5 additions x 35 = 1813)
-        "miller": 4400 * 4040 / 5853,
+        # Miller loop, 4400 FME per pair: all of it in the fused kernel, or split between the two kernels of
+        # the split form in proportion to the products each executes per pair: k_miller_acc4<2> (f shared by two
+        # pairs: 62 Fp12 squarings x 36 / 2 + 68 sparse line products x 43 = 4040) and k_miller_lines2 (T: 63
+        # doublings x 26 + 5 additions x 35 = 1813).  (The MSM's 64 extra pairs per batch are not counted.)
+        "miller": 4400 if MILLER_FUSED else 4400 * 4040 / 5853,
         "miller_lines": 4400 * 1813 / 5853,
     }
 

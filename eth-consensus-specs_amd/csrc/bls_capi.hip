@@ -23,10 +23,10 @@ enum Slot {
   // FAV batch state (kept between partial and finish)
   S_FAV_F, S_FAV_FT, S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
-  S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD, S_BSIG, S_BRSC, S_BLINES,
+  S_BP, S_BQ, S_BS, S_BT, S_BSEL, S_BRES, S_BBAD, S_BSIG, S_BRSC,
   // AggregateVerify batches (own slots: a FAV batch may be between its partial and finish calls)
   S_AV_IO, S_AV_RSC, S_AV_PITEM, S_AV_SIG, S_AV_SOK, S_AV_H, S_AV_ST, S_AV_P, S_AV_Q, S_AV_F, S_AV_FT, S_AV_SEL,
-  S_AV_FI, S_AV_RES, S_AV_HCF, S_AV_FLAG, S_AV_ML,
+  S_AV_FI, S_AV_RES, S_AV_HCF, S_AV_FLAG,
   // signing roots / merkleization
   S_SZ_A, S_SZ_B, S_SZ_C, S_SZ_Z,
   // KZG pieces
@@ -1032,6 +1032,16 @@ int bls_profile_read(bls_ctx* ctx, double* total_ms, uint64_t* counts, int max) 
 const char* bls_profile_name(int i) { return (i >= 0 && i < PROF_N) ? PROF_NAMES[i] : ""; }
 
 // ---------------------------------------------------------- FAV batches --
+// A FAV batch's Miller loops run split -- the line kernel on stream2 right after the hash, the f accumulation on
+// stream1 -- or, with BLS_MILLER_FUSED=1, as one fused kernel (k_miller_fused).  The fused kernel holds a SIMD per
+// line wave for the whole loop, so per batch it costs more SIMD time than the two kernels at full occupancy (C2
+// 2.32 -> 2.14 M FAV/s, C3 1.51 -> 1.46 M: profiles/r05o_miller_fused_ab.txt) although its launch alone runs the
+// Miller loop at 0.0995 of peak against the accumulation kernel's 0.070; the latency-bound callers -- the
+// bisection's per-item values and AggregateVerify batches -- always take it.
+static bool miller_fused() {
+  static const bool on = getenv("BLS_MILLER_FUSED") && !strcmp(getenv("BLS_MILLER_FUSED"), "1");
+  return on;
+}
 constexpr size_t ACC_SHARED_MIN = 4096;  // items per FAV batch from which k_miller_acc4q shares f between two pairs
 
 static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offs, size_t B, const uint8_t* d_msgs,
@@ -1065,8 +1075,8 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   SCR(S_RPJ, B, rpj);
   // Miller loop of all NP pairs, split: G2 lines (k_miller_lines2) on stream2 after hash_to_G2 and the MSM, f
   // accumulated on stream1 by k_miller_acc4q (four lanes per f, G pairs per f: one squaring per step for all G)
-  uint32_t* mlines;
-  SCR(S_MLINES, miller_lines_u32(NP), mlines);
+  uint32_t* mlines = nullptr;
+  if (!miller_fused()) SCR(S_MLINES, miller_lines_u32(NP), mlines);
   SCR(S_MSTAT, B, dstat);
   SCR(S_FAV_F, NP, f);  // per-item (or per-group) f, kept for the bisection: not S_F, which per-call checks use
   SCR(S_FAV_FT, NP / 8 + 16, ft);
@@ -1117,19 +1127,28 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   if (!two) HIPCK(hipStreamWaitEvent(sm, J.ev_gather, 0));
   PROF2(11, sm, launch_msm_upairs(sm, B, gstat, dstat, rsc, sig, msmu, msmf, ctx->comb, rP + B, H + B, status + B));
   HIPCK(hipEventRecord(J.ev_msm, sm));
-  // the lines of every pair: the hashes' (stream2) and the MSM's (ev_msm)
-  HIPCK(hipStreamWaitEvent(st2, J.ev_msm, 0));
-  PROF2(12, st2, launch_miller_lines(st2, H, NP, mlines));
+  // the Miller loops of all NP pairs: one fused kernel (k_miller_fused, lines in LDS) on stream1 after the hash, or
+  // (BLS_MILLER_FUSED=0) the G2 lines on stream2 after the hash and the MSM, then the f accumulation on stream1
+  const bool fused = miller_fused();
+  if (!fused) {
+    HIPCK(hipStreamWaitEvent(st2, J.ev_msm, 0));
+    PROF2(12, st2, launch_miller_lines(st2, H, NP, mlines));
+  }
   HIPCK(hipEventRecord(J.ev_join, st2));
   if (!two) HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   PROF(10, launch_sig_vm(st, B, gstat, status, dstat, apka, sig, rsc, rpj, rP));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
+  if (fused && !two) HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
   // two pairs share each f (one squaring per step for both) on full batches; below ACC_SHARED_MIN items the
   // launch under-fills the chip and the chain latency is what counts, so one pair per f (a step is a squaring
   // and ONE line: ~37 % shorter chains for ~24 % more products)
-  const int mg = B >= ACC_SHARED_MIN ? 2 : 1;
+  static const int acc_g = getenv("BLS_ACC_G") ? atoi(getenv("BLS_ACC_G")) : 2;  // pairs per f of full batches
+  const int mg = B >= ACC_SHARED_MIN ? (acc_g == 4 ? 4 : 2) : 1;
   J.fav_mg = mg;
-  PROF(5, launch_miller_acc4(st, rP, H, status, NP, mlines, NP, f, mg));
+  if (fused)
+    PROF(5, launch_miller_fused(st, rP, H, status, NP, f, mg));
+  else
+    PROF(5, launch_miller_acc4(st, rP, H, status, NP, mlines, NP, f, mg));
   PROF(6, launch_fp12_prod_vm(st, f, (NP + mg - 1) / mg, ft, fo));
   J.fav_B = B;
   J.fav_ready = true;
@@ -1166,7 +1185,6 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   const G2A* H = (const G2A*)J.buf[S_H].p;
   const G2A* sig0 = (const G2A*)J.buf[S_SIG].p;
   Fp12* fb = (Fp12*)J.buf[S_FAV_F].p;
-  const uint32_t* mlines = (const uint32_t*)J.buf[S_MLINES].p;
   std::vector<size_t> off{0}, cnt{B};
   while (cnt.back() > 1) {
     off.push_back(off.back() + cnt.back());
@@ -1181,7 +1199,7 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   G1P* Pj;
   Fp12 *fS, *fH, *tree;
   int* res;
-  uint32_t *nchk, *slines;
+  uint32_t* nchk;
   G2A* sig;
   uint64_t* rsc;
   SCR(S_BP, B, Ps);
@@ -1192,20 +1210,19 @@ static int fav_bisect(bls_ctx* ctx, bool root_bad, uint8_t* d_out) {
   SCR(S_BBAD, 1, nchk);
   SCR(S_BSIG, B, sig);
   SCR(S_BRSC, B, rsc);
-  SCR(S_BLINES, miller_lines_u32(B), slines);
+
   if (J.fav_mg > 1) SCR(S_BSEL, B, fH);
   else fH = fb;
   hipStream_t st = J.stream;
   // first everything read of the state that the job's next batch writes from stream2 / stream3 (H and the line
   // records, sigma_i, r_i); that batch forks from ev_bis (fav_prepare) while the rest runs here
-  if (J.fav_mg > 1) LK(launch_miller_acc4(st, rP, H, status, B, mlines, B + MSM_UPAIRS, fH, 1));
+  if (J.fav_mg > 1) LK(launch_miller_fused(st, rP, H, status, B, fH, 1));
   HIPCK(hipMemcpyAsync(sig, sig0, B * sizeof(G2A), hipMemcpyDeviceToDevice, st));
   HIPCK(hipMemcpyAsync(rsc, rsc0, B * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   HIPCK(hipEventRecord(J.ev_bis, st));
   J.bis_pending = true;
   LK(launch_neg_rg1(st, B, status, rsc, ctx->comb, Pj, Ps));
-  LK(launch_miller_lines(st, sig, B, slines));
-  LK(launch_miller_acc4(st, Ps, sig, status, B, slines, B, fS, 1));
+  LK(launch_miller_fused(st, Ps, sig, status, B, fS, 1));
   LK(launch_fp12_chunk_prod2(st, fH, fS, B, 1, tree));
   for (int L = 0; L < top; L++) LK(launch_fp12_chunk_prod(st, tree + off[L], cnt[L], 16, tree + off[L + 1]));
   HIPCK(hipMemsetAsync(nchk, 0, sizeof(uint32_t), st));
@@ -1424,12 +1441,9 @@ int bls_aggregate_verify_batch(bls_ctx* ctx, const uint8_t* pks48, const uint8_t
   }
   LK(launch_av_items(st, B, d_io, d_pok, d_sok, d_sa, d_rsc, d_status, P2, Q2));
   LK(launch_av_pairs(st, total, d_pitem, d_status, d_rsc, d_pa, d_h, P2, Q2));
-  if (npair >= 256) {  // per-pair Miller values (the fallback multiplies each item's segment): G2 lines, then
-                       // f accumulated by four lanes per pair (bls_miller_pair.hip, G = 1)
-    uint32_t* mlines;
-    SCR(S_AV_ML, miller_lines_u32(npair), mlines);
-    LK(launch_miller_lines(st, Q2, npair, mlines));
-    PROF(5, launch_miller_acc4(st, P2, Q2, nullptr, npair, mlines, npair, f, 1));
+  if (npair >= 256) {  // per-pair Miller values (the fallback multiplies each item's segment): the fused kernel
+                       // (G2 lines and f accumulation in one workgroup, bls_miller_pair.hip, G = 1)
+    PROF(5, launch_miller_fused(st, P2, Q2, nullptr, npair, f, 1));
   } else {
     PROF(5, launch_miller_wave(st, P2, Q2, nullptr, npair, f));
   }

@@ -1,8 +1,11 @@
 // f accumulation of the split Miller loop (the G2 side, k_miller_lines2 in
 // bls_miller_lane.hip, writes the line records) with four lanes per f, in the
 // bound-typed redundant digit form (bls_fqb.h).
+#include <type_traits>
+
 #include "bls_fqb.h"
 #include "bls_kernels.h"
+#include "bls_miller_lines.h"
 #include "bls_tower_inline.h"
 
 namespace bls {
@@ -172,6 +175,26 @@ __device__ __forceinline__ LineIn ld_line(const uint32_t* Li, size_t n, bool h, 
   return r;
 }
 
+// a P-scaled record of k_miller_fused's line wave (mlines::Line1/Line2<true>): l0, l2 = E ZZ (-x_P), l3 = z3 ZZ y_P
+// (l2 and l3 are products -- mlines::scale -- so their words are N-form digits)
+struct LineS {
+  Fq2B<ML_LV, ML_LD> l0;
+  Fq2B<2, fqb_detail::MASK> l2, l3;
+};
+__device__ __forceinline__ LineS ld_line_s(const uint32_t* Li, size_t n) {
+  LineS r;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    r.l0.c0.x.d[j] = Li[(size_t)j * n];
+    r.l0.c1.x.d[j] = Li[(size_t)(14 + j) * n];
+    r.l2.c0.x.d[j] = Li[(size_t)(28 + j) * n];
+    r.l2.c1.x.d[j] = Li[(size_t)(42 + j) * n];
+    r.l3.c0.x.d[j] = Li[(size_t)(56 + j) * n];
+    r.l3.c1.x.d[j] = Li[(size_t)(70 + j) * n];
+  }
+  return r;
+}
+
 // the line's P factors, as q_line_p: l2 = E ZZ (-x_P), l3 = z3 ZZ y_P in N form
 template <uint64_t VP, uint64_t DP>
 __device__ __forceinline__ void qq_line_p(const LineIn& in, const FqB<VP, DP>& pc, bool q, Fq2B<2, fqb_detail::MASK>& l2,
@@ -222,8 +245,12 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
   F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
   // the P coordinate each lane scales its line coefficient by: -x_P (h = 0, as K - x_P) or y_P (h = 1), once
   // (two named values, not an array: the pair loop is not unrolled and an indexed array went to scratch)
-  const FqC pa = fqb_canon(h ? P[pi[0]].y : P[pi[0]].x), pb = fqb_canon(h ? P[pi[G - 1]].y : P[pi[G - 1]].x);
+  // (named values, not an array: the pair loop is unrolled but an indexed array went to scratch)
+  const FqC pa = fqb_canon(h ? P[pi[0]].y : P[pi[0]].x), pb = fqb_canon(h ? P[pi[G > 1 ? 1 : 0]].y : P[pi[G > 1 ? 1 : 0]].x);
+  const FqC pc_ = fqb_canon(h ? P[pi[G > 2 ? 2 : 0]].y : P[pi[G > 2 ? 2 : 0]].x);
+  const FqC pd_ = fqb_canon(h ? P[pi[G > 3 ? 3 : 0]].y : P[pi[G > 3 ? 3 : 0]].x);
   const auto pc0 = sel(h, pa, zero - pa), pc1 = sel(h, pb, zero - pb);
+  const auto pc2 = sel(h, pc_, zero - pc_), pc3 = sel(h, pd_, zero - pd_);
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = relax<VF, DF>(qq_sqr(f, h, q));
@@ -234,7 +261,7 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
       for (int g = 0; g < G; ++g) {
         const LineIn cur = ld_line(Lb[g], ld, h, q);
         Fq2B<2, fqb_detail::MASK> l2, l3;
-        qq_line_p(cur, sel(g == 0, pc0, pc1), q, l2, l3);
+        qq_line_p(cur, g == 0 ? pc0 : (g == 1 ? pc1 : (g == 2 ? pc2 : pc3)), q, l2, l3);
         const auto fl = relax<VF, DF>(qq_line(f, h, q, cur.l0, l2, l3));
         f = G == 1 ? fl : sel(live[g], fl, f);
         Lb[g] += step;
@@ -250,13 +277,138 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_miller_fused<G>: both halves of the split Miller loop in ONE workgroup per MF_PAIRS<G> pairs.  Wave 0 runs
+// the G2 side and writes each line record into an LDS double buffer; waves 1 and 2 run the f accumulation (four
+// lanes per f, G pairs per f, the code of k_miller_acc4q) and read the record of line k while wave 0 forms line k
+// + 1 -- one workgroup barrier per line (68).  The line wave is sized to keep up with the accumulation waves:
+//   G = 2: 64 pairs, mlines::Line1 (one lane per pair); two accumulation waves of 16 f x 2 pairs
+//   G = 1: 32 pairs, mlines::Line2 (two lanes per pair); two accumulation waves of 16 f x 1 pair
+// (G = 2 with two lanes per pair and one accumulation wave waited at the barrier half the time: C2 -12 %.)
+// Three waves per workgroup: each keeps the whole register file of its SIMD.  The records never touch
+// HBM (split into k_miller_lines2 + k_miller_acc4q, a C2 batch wrote and read 84 words x 68 lines per pair, 228
+// MB each way), the line kernel's latency leaves the batch's chain, and the launch puts twice the waves of the
+// accumulation alone on the chip.
+template <int G>
+constexpr int MF_PAIRS = G == 2 ? 64 : 32;
+template <int G>
+constexpr int MF_ACC = 4 * MF_PAIRS<G> / G / 64;  // f-accumulation waves per workgroup (two)
+
+template <int G>
+__global__ void __launch_bounds__(64 * (1 + MF_ACC<G>)) k_miller_fused(const G1A* P, const G2A* Q, const int* ok,
+                                                                       size_t n, Fp12* out) {
+  constexpr int PW = MF_PAIRS<G>;
+  __shared__ uint32_t rec[2][ML_WORDS * PW];
+  __shared__ uint32_t qlds[56 * 64];
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const size_t pair0 = (size_t)blockIdx.x * PW;
+  if (wave == 0) {  // ---- G2 side: line k + 1 while the accumulation reads line k
+    constexpr int LPP = 64 / PW;  // lanes per pair
+    const int pl = lane / LPP;
+    const size_t i = pair0 + pl < n ? pair0 + pl : n - 1;
+    G2A q = Q[i];
+    if (q.inf) q = g2_generator();  // its records are read but not used (the pair is not live)
+    using LT = typename std::conditional<LPP == 1, mlines::Line1<true>, mlines::Line2<true>>::type;
+    LT T;
+    if constexpr (LPP == 1)
+      T.init(q, qlds, lane);
+    else
+      T.init(q, (lane & 1) != 0, qlds, lane);
+    T.pf.init(P[i]);  // the records carry l2, l3 with the pair's P factors applied
+    uint32_t* const r0 = &rec[0][pl];
+    uint32_t* const r1 = &rec[1][pl];
+    T.dbl(r0, PW);  // line 0: the doubling at b = 62
+    __syncthreads();
+    int b = 62;
+    bool added = false;  // whether the record of bit b's addition step has been written
+#pragma unroll 1
+    for (int k = 1; k <= MILLER_NLINES; ++k) {
+      if (k < MILLER_NLINES) {
+        uint32_t* dst = (k & 1) ? r1 : r0;
+        if (!added && ((X_ABS >> b) & 1ull)) {
+          T.add(dst, PW, qlds, lane);
+          added = true;
+        } else {
+          --b;
+          added = false;
+          T.dbl(dst, PW);
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // ---- f accumulation: lanes 4k + 2h + q of the accumulation waves own f k of the workgroup (pairs G k .. G k +
+  // G - 1 of its MF_PAIRS); every lane runs the whole loop (the barriers), out-of-range groups write nothing
+  const int at = (wave - 1) * 64 + lane;
+  const int grp = at >> 2;
+  const bool h = (at & 2) != 0, q = (at & 1) != 0;
+  bool live[G];
+  int pl[G];
+  size_t pi[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    pl[g] = grp * G + g;
+    const size_t p = pair0 + pl[g];
+    pi[g] = p < n ? p : n - 1;
+    live[g] = p < n && (!ok || ok[p]) && !P[pi[g]].inf && !Q[pi[g]].inf;
+  }
+  constexpr uint64_t VF = ML_QF_V, DF = ML_QF_D;
+  using F = Fq6B<VF, DF>;
+  const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
+  const Fq2B<1, fqb_detail::MASK> z2{zero, zero};
+  F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
+  __syncthreads();  // line 0 is in rec[0]
+  int k = 0;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = relax<VF, DF>(qq_sqr(f, h, q));
+    const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
+#pragma unroll 1
+    for (int s = 0; s < nl; ++s, ++k) {
+      const uint32_t* buf = rec[k & 1];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const LineS cur = ld_line_s(buf + pl[g], PW);
+        const auto fl = relax<VF, DF>(qq_line(f, h, q, cur.l0, cur.l2, cur.l3));
+        f = sel(live[g], fl, f);
+      }
+      __syncthreads();
+    }
+  }
+  const size_t og = pair0 / G + grp;
+  if (q || og >= (n + G - 1) / G) return;
+  bool any = false;
+#pragma unroll
+  for (int g = 0; g < G; ++g) any = any || live[g];
+  Fp6 r{fq2b_pack(f.c0), fq2b_pack(f.c1), fq2b_pack(f.c2)};
+  if (!any) r = h ? Fp6{fp2_zero(), fp2_zero(), fp2_zero()} : Fp6{fp2_one(), fp2_zero(), fp2_zero()};
+  if (h)
+    out[og].c1 = Fp6{fp2_neg(r.c0), fp2_neg(r.c1), fp2_neg(r.c2)};
+  else
+    out[og].c0 = r;
+}
+
+hipError_t launch_miller_fused(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f, int G) {
+  if (!n) return hipSuccess;
+  if (G == 2)
+    hipLaunchKernelGGL(k_miller_fused<2>, dim3((unsigned)((n + MF_PAIRS<2> - 1) / MF_PAIRS<2>)),
+                       dim3(64 * (1 + MF_ACC<2>)), 0, st, P, Q, ok, n, f);
+  else
+    hipLaunchKernelGGL(k_miller_fused<1>, dim3((unsigned)((n + MF_PAIRS<1> - 1) / MF_PAIRS<1>)),
+                       dim3(64 * (1 + MF_ACC<1>)), 0, st, P, Q, ok, n, f);
+  return hipGetLastError();
+}
+
 hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                               size_t ld, Fp12* f, int G) {
   if (!n) return hipSuccess;
   if (ld < n) return hipErrorInvalidValue;
   const size_t ngrp = (n + G - 1) / G;
   const dim3 grid((unsigned)((4 * ngrp + 63) / 64));
-  if (G == 2)
+  if (G == 4)
+    hipLaunchKernelGGL(k_miller_acc4q<4>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
+  else if (G == 2)
     hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   else
     hipLaunchKernelGGL(k_miller_acc4q<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
