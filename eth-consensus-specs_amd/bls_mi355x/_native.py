@@ -86,6 +86,7 @@ _SIGS = {
     "bls_fav_job_partial": (_ip, [_vp, _ip, _vp]),
     "bls_fav_job_check": (_ip, [_vp, _ip, _u8p, _sz]),
     "bls_fav_job_check_own": (_ip, [_vp, _ip]),
+    "bls_test_miller_forms": (_ip, [_vp, _u8p, _u8p, _sz, _u8p]),
     "bls_fav_job_finish_dev": (_ip, [_vp, _ip, _ip, _vp]),
     "bls_registry_generate": (_ip, [_vp, ctypes.c_uint64, _sz, _vp]),
     "bls_last_fallback_stats": (_ip, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),

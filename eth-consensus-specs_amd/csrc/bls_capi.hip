@@ -881,6 +881,60 @@ int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out) {
   return 0;
 }
 
+// The product of n pairings through each Miller-loop form of the batch path, final-exponentiated: out576[576 k ..]
+// for form k = 0 split (k_miller_lines2 + k_miller_acc4q<2>), 1 fused G = 2, 2 fused G = 1, 3 split G = 4, 4 the
+// wave-program kernel (the reference form of bls_multi_pairing).  Points are decoded without subgroup checks;
+// identity points are skipped pairs.  Returns 1, or 0 if an encoding is invalid.
+int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, uint8_t* out576) {
+  API_ENTER(ctx);
+  if (!n || !g1s48 || !g2s96 || !out576) return BLS_E_ARG;
+  hipStream_t st = ctx->j->stream;
+  uint8_t *d_in, *d_out;
+  G1A* P;
+  G2A* Q;
+  int *ok1, *ok2;
+  Fp12 *f, *ft, *fo;
+  uint32_t* L;
+  SCR(S_KZ_IN, 144 * n, d_in);
+  SCR(S_KZ_P, n, P);
+  SCR(S_KZ_Q, n, Q);
+  SCR(S_KZ_OK, n, ok1);
+  SCR(S_KZ_OK2, n, ok2);
+  SCR(S_KZ_F, n, f);
+  SCR(S_KZ_FT, n / 8 + 16, ft);
+  SCR(S_FPART, 1, fo);
+  SCR(S_PT_OUT, 5 * 576, d_out);
+  SCR(S_KZ_J, miller_lines_u32(n), L);
+  CK(h2d(ctx, d_in, g1s48, 48 * n));
+  CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
+  LK(launch_pt_decode(st, 1, d_in, n, 0, P, ok1));
+  LK(launch_pt_decode(st, 2, d_in + 48 * n, n, 0, Q, ok2));
+  std::vector<int> a(n), b(n);
+  CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
+  CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
+  for (size_t i = 0; i < n; i++)
+    if (!a[i] || !b[i]) return 0;
+  for (int k = 0; k < 5; ++k) {
+    size_t nf = n;
+    if (k == 0 || k == 3) {
+      const int G = k == 0 ? 2 : 4;
+      LK(launch_miller_lines(st, Q, n, L));
+      LK(launch_miller_acc4(st, P, Q, nullptr, n, L, n, f, G));
+      nf = (n + G - 1) / G;
+    } else if (k == 1 || k == 2) {
+      const int G = k == 1 ? 2 : 1;
+      LK(launch_miller_fused(st, P, Q, nullptr, n, f, G));
+      nf = (n + G - 1) / G;
+    } else {
+      LK(launch_miller_wave(st, P, Q, nullptr, n, f));
+    }
+    LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
+    LK(launch_gt_final_exp(st, fo, d_out + 576 * k));
+  }
+  CK(d2h(ctx, out576, d_out, 5 * 576));
+  return 1;
+}
+
 int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96) {
   API_ENTER(ctx);
   if ((!msgs32 || !out96) && n) return BLS_E_ARG;
