@@ -919,7 +919,7 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
     if (k == 0 || k == 3) {
       const int G = k == 0 ? 2 : 4;
       LK(launch_miller_lines(st, Q, n, L));
-      LK(launch_miller_acc4(st, P, Q, nullptr, n, L, n, f, G));
+      LK(launch_miller_acc4(st, P, Q, nullptr, n, L, miller_lines_ld(n), f, G));
       nf = (n + G - 1) / G;
     } else if (k == 1 || k == 2) {
       const int G = k == 1 ? 2 : 1;
@@ -1202,7 +1202,7 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   if (fused)
     PROF(5, launch_miller_fused(st, rP, H, status, NP, f, mg));
   else
-    PROF(5, launch_miller_acc4(st, rP, H, status, NP, mlines, NP, f, mg));
+    PROF(5, launch_miller_acc4(st, rP, H, status, NP, mlines, miller_lines_ld(NP), f, mg));
   PROF(6, launch_fp12_prod_vm(st, f, (NP + mg - 1) / mg, ft, fo));
   J.fav_B = B;
   J.fav_ready = true;

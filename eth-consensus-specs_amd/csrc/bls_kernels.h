@@ -69,6 +69,7 @@ constexpr int MILLER_NLINES = 68;  // 63 doublings + 5 additions (|x| = 0xd20100
 // ML_LD), word w of line k of pair i at L[(k * ML_WORDS + w) * n + i]
 constexpr int ML_WORDS = 84;
 constexpr uint64_t ML_LV = 4096, ML_LD = 0x20000000ull + 64;
+size_t miller_lines_ld(size_t n);  // the records' leading dimension (>= n, a multiple of 32 pairs)
 size_t miller_lines_u32(size_t n);
 hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L);
 // four lanes per f, G = 1 or 2 pairs per f (bls_miller_pair.hip); writes ceil(n / G) values; ld >= n: the

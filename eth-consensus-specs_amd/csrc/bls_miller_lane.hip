@@ -22,7 +22,7 @@ namespace bls {
 // FqB<ML_LV, ML_LD> (bls_fqb.h), which the accumulation multiplies without unpacking.
 //
 // TWO lanes per pair: the step code is mlines::Line2 (bls_miller_lines.h), shared with k_miller_fused.
-__global__ void __launch_bounds__(64) k_miller_lines2(const G2A* Q, size_t n, uint32_t* L) {
+__global__ void __launch_bounds__(64) k_miller_lines2(const G2A* Q, size_t n, size_t ld, uint32_t* L) {
   const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
   const size_t i = t >> 1;
   if (i >= n) return;  // both lanes of a pair leave together
@@ -32,23 +32,29 @@ __global__ void __launch_bounds__(64) k_miller_lines2(const G2A* Q, size_t n, ui
   mlines::Line2<> T;
   T.init(q, (t & 1) != 0, qlds, (int)threadIdx.x);
   uint32_t* Li = L + i;
-  const size_t step = (size_t)ML_WORDS * n;
+  const size_t step = (size_t)ML_WORDS * ld;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
-    T.dbl(Li, n);
+    T.dbl(Li, ld);
     Li += step;
     if ((X_ABS >> b) & 1ull) {
-      T.add(Li, n, qlds, (int)threadIdx.x);
+      T.add(Li, ld, qlds, (int)threadIdx.x);
       Li += step;
     }
   }
 }
 
-size_t miller_lines_u32(size_t n) { return (size_t)MILLER_NLINES * ML_WORDS * n; }
+// the leading dimension of n pairs' records: a multiple of 32 pairs, so every record row starts on a 128-B line.
+// (With ld = n a row started 64 B into a line whenever n = 16 mod 32 -- a C2 batch of 10,064 pairs -- and the
+// line straddling two workgroups' 32-pair spans was fetched once per XCD: FETCH 1.50x the record bytes for
+// k_miller_acc4q<2>, reproduced by tools/microbench/fetchcal.hip.)
+size_t miller_lines_ld(size_t n) { return (n + 31) & ~(size_t)31; }
+size_t miller_lines_u32(size_t n) { return (size_t)MILLER_NLINES * ML_WORDS * miller_lines_ld(n); }
 
 hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t* L) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_miller_lines2, dim3((unsigned)((2 * n + 63) / 64)), dim3(64), 0, st, Q, n, L);
+  hipLaunchKernelGGL(k_miller_lines2, dim3((unsigned)((2 * n + 63) / 64)), dim3(64), 0, st, Q, n, miller_lines_ld(n),
+                     L);
   return hipGetLastError();
 }
 
