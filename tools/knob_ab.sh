@@ -13,7 +13,7 @@ for r in $(seq 1 $REPS); do
     envs=""; [ "$kv" != base ] && envs="$kv"
     env $envs timeout -k 10 150 python3 bench.py --steps $STEPS --warmup 3 --no-cpu --no-percall --no-e2e --roofline-passes 2 --c4-steps 0 --c5-steps 0 --no-regload \
       > $OUT/k${i}_r$r.json 2> $OUT/k${i}_r$r.err || { echo "[$kv] FAILED rc=$?"; tail -3 $OUT/k${i}_r$r.err | cut -c1-300; exit 1; }
-    python3 -c "import json; d=json.load(open('$OUT/k${i}_r$r.json')); print('[$kv] r$r', d['value'], (d.get('c3') or {}).get('fav_s'))"
+    python3 -c "import json; d=json.load(open('$OUT/k${i}_r$r.json')); print('[$kv] r$r', d['value'], (d.get('c3') or {}).get('fav_s'), 'frac', d['roofline']['frac'], 'launch_ms', d['roofline']['avg_launch_ms'])"
   done
 done
 i=0
