@@ -27,11 +27,6 @@ def _ctx():
     return _native.context()
 
 
-def _cat(items, width):
-    out = b"".join(_b(x) for x in items)
-    return out
-
-
 class mi355x_bls:  # noqa: N801 -- mirrors the reference's backend class naming
     """Backend object assigned to ``bls`` by ``use_mi355x()``."""
 

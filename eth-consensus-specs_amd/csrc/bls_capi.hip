@@ -1181,8 +1181,8 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   if (!two) HIPCK(hipStreamWaitEvent(sm, J.ev_gather, 0));
   PROF2(11, sm, launch_msm_upairs(sm, B, gstat, dstat, rsc, sig, msmu, msmf, ctx->comb, rP + B, H + B, status + B));
   HIPCK(hipEventRecord(J.ev_msm, sm));
-  // the Miller loops of all NP pairs: one fused kernel (k_miller_fused, lines in LDS) on stream1 after the hash, or
-  // (BLS_MILLER_FUSED=0) the G2 lines on stream2 after the hash and the MSM, then the f accumulation on stream1
+  // the Miller loops of all NP pairs: the G2 lines on stream2 after the hash and the MSM, then the f accumulation on
+  // stream1 -- or (BLS_MILLER_FUSED=1) one fused kernel (k_miller_fused, lines in LDS) on stream1
   const bool fused = miller_fused();
   if (!fused) {
     HIPCK(hipStreamWaitEvent(st2, J.ev_msm, 0));
@@ -1214,11 +1214,10 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
 // per-signature bisection"), on the job's own stream with no host round trip.
 // The leaves are the items' Miller values from the batch's own kernels:
 //   f_H,i   = ML(r_i apk_i, H_i): the batch's per-item f (one pair per f below
-//             ACC_SHARED_MIN items) or k_miller_acc4q<1> over the batch's line
-//             records again (shared-f batches);
+//             ACC_SHARED_MIN items) or k_miller_fused<1> over the batch's
+//             r_i apk_i and H_i again (shared-f batches);
 //   f_sig,i = ML(-r_i G1, sigma_i): -r_i G1 from a fixed-base comb (8 mixed
-//             additions), sigma_i's line records by k_miller_lines2, f by
-//             k_miller_acc4q<1>;
+//             additions, k_neg_rg1), f by k_miller_fused<1>;
 // leaf_i = f_H,i f_sig,i, and a 16-ary product tree above the leaves.  A node's
 // check is FE(node) == 1: the product of e(r_i apk_i, H_i) e(-r_i G1, sigma_i)
 // over its items, the random linear combination of their checks.  The first

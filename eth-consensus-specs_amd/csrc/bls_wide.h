@@ -27,7 +27,7 @@
 //   4. T + m p (14 more steps), normalised: the low 14 digits then sum to 0 or
 //      exactly R (they are = 0 mod R and below 2 R), so the carry into digit 14
 //      is "any low digit nonzero" -- one wave ballot, no carry chain.
-//   5. digits 14..27 move down to lanes 0..13 of both rows (ds_bpermute).
+//   5. digits 14..27 move down to lanes 0..13 of both rows (v_permlane16_swap + two DPP row shifts: whigh).
 // ~140 wave instructions per product pair instead of ~500 per lane product:
 // ~3.5x lower latency per product, ~8x per Fp2 product (wdot2 forms a whole
 // Fp2 coefficient with one reduction).  Nothing is sequential across digits
@@ -111,6 +111,20 @@ __device__ __forceinline__ void wmac(uint64_t& acc, uint32_t x, uint32_t y) {
   });
 }
 
+// columns 14..27 of a half (lanes 14, 15 of its first row, 0..11 of its second) -> digits 0..13 of BOTH rows, lanes
+// 14, 15 zero (columns 28, 29 are zero: the value is below 2^(29 x 28)).  v_permlane16_swap puts the first row's
+// columns in both rows of one register and the second row's in both rows of another; row_shl:14 / row_shr:2 (zero
+// fill) then line them up -- four VALU operations where a ds_bpermute cost ~250 cycles of LDS-path latency on the
+// chain (tools/microbench/widerate.hip).
+__device__ __forceinline__ uint32_t whigh(uint32_t u) {
+  const auto sw = __builtin_amdgcn_permlane16_swap(u, u, false, false);  // [0]: first rows, [1]: second rows
+  uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)sw[0], 0x10E, 0xF, 0xF, true);  // row_shl:14
+  uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)sw[1], 0x112, 0xF, 0xF, true);  // row_shr:2
+  BLS_WIDE_FENCE(a);
+  BLS_WIDE_FENCE(b);
+  return a | b;  // disjoint lanes
+}
+
 // Montgomery reduction of column sums (< 2^63, value T < p R): T R^-1 mod p in W form (value < 2.0001 p)
 __device__ __forceinline__ uint32_t wredc(uint64_t acc) {
   const int k = wpos();
@@ -136,9 +150,7 @@ __device__ __forceinline__ uint32_t wredc(uint64_t acc) {
   const uint64_t bal = __builtin_amdgcn_ballot_w64(k < 14 && u != 0u);
   const bool lowc = ((bal >> (threadIdx.x & 32u)) & 0x3fffull) != 0;
   const uint32_t u2 = u + ((k == 14 && lowc) ? 1u : 0u);
-  const int j = wdig();
-  const int src = (int)(threadIdx.x & 32u) + (j < 14 ? 14 + j : 31);  // lane 31 of a half is always 0
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)u2);
+  return whigh(u2);
 }
 
 __device__ __forceinline__ uint32_t wmul(uint32_t x, uint32_t y) {
@@ -220,8 +232,10 @@ __device__ __forceinline__ Fp w_to_fp(uint32_t v) { return fq_pack(w_to_fq(v)); 
 __device__ __forceinline__ bool w_is_zero(uint32_t v) { return fp_is_zero(w_to_fp(v)); }
 __device__ __forceinline__ bool w_eq(const WK& K, uint32_t a, uint32_t b) { return w_is_zero(wsub(K, a, b)); }
 // the other half's value (lane l gets lane l ^ 32)
+// (v_permlane32_swap: [0] holds the first half in both halves, [1] the second; a VALU move, not the LDS path)
 __device__ __forceinline__ uint32_t wswap(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ 32u) & 63u) << 2, (int)v);
+  const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return whalf() ? (uint32_t)sw[0] : (uint32_t)sw[1];
 }
 
 // a^e for a fixed exponent (little-endian u32 limbs, bit nbits-1 set), sliding window w = 3 (as fq_pow_w3)
@@ -285,7 +299,7 @@ __device__ __forceinline__ W2 w2sel(bool c, W2 a, W2 b) { return W2{c ? a.c0 : b
 
 // ---- Fp2 in F2 layout: one VGPR, c0 in half 0 and c1 in half 1 (D layout each) ----
 // An Fp2 product is ONE wdot2 per half (both halves at once): half 0 forms c0 = a0 b0 + a1 (kn - b1), half 1
-// c1 = a0 b1 + a1 b0, each reading the other half's coefficients through one ds_bpermute (wswap).  kn is a
+// c1 = a0 b1 + a1 b0, each reading the other half's coefficients through one v_permlane32_swap (wswap).  kn is a
 // multiple of p in borrowed digits covering b1 (the 4096p of bls_fq_g2.h for b1 < 4096p).
 __device__ __forceinline__ uint32_t wf_mul(uint32_t kn, uint32_t a, uint32_t b) {
   const bool h = whalf() != 0;

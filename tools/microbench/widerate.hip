@@ -6,7 +6,12 @@
 #include <stdio.h>
 
 #include "bls_fq.h"
+#include "bls_h2c.h"
+#include "bls_kernels.h"
+#include "bls_lane.h"
 #include "bls_wide.h"
+#include "bls_wide_g2.h"
+#include "bls_xmd32.h"
 
 using namespace bls;
 using namespace bls::wide;
@@ -72,6 +77,157 @@ __device__ __forceinline__ uint32_t wredc2(uint64_t acc) {
   const int src = (int)(threadIdx.x & 32u) + (j < 14 ? 14 + j : 31);
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)u2);
 }
+// the round-4 reduction: the high digits moved down by one ds_bpermute (whigh's predecessor)
+__device__ __forceinline__ uint32_t wredc_bp(uint64_t acc) {
+  const int k = wpos();
+  const uint32_t t = wnorm64(acc);
+  uint64_t am = 0;
+  uint32_t s = k < 14 ? t : 0u;
+  for14([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (i) s = shr1(s);
+    am += (uint64_t)NINV29[i] * s;
+  });
+  const uint32_t mn = wnorm64(am);
+  const uint32_t m = k < 14 ? mn : 0u;
+  uint64_t au = t;
+  s = m;
+  for14([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (i) s = shr1(s);
+    au += (uint64_t)P29[i] * s;
+  });
+  const uint32_t u = wnorm64(au);
+  const uint64_t bal = __builtin_amdgcn_ballot_w64(k < 14 && u != 0u);
+  const bool lowc = ((bal >> (threadIdx.x & 32u)) & 0x3fffull) != 0;
+  const uint32_t u2 = u + ((k == 14 && lowc) ? 1u : 0u);
+  const int j = wdig();
+  const int src = (int)(threadIdx.x & 32u) + (j < 14 ? 14 + j : 31);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)u2);
+}
+__device__ __forceinline__ uint32_t wmul_bp(uint32_t x, uint32_t y) {
+  uint64_t a = 0;
+  wmac(a, x, y);
+  return wredc_bp(a);
+}
+__device__ __forceinline__ uint32_t wswap_bp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x ^ 32u) & 63u) << 2, (int)v);
+}
+__global__ void __launch_bounds__(64) k_wmul_bp(uint32_t* out, int iters) {
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32)), y = w_from_fp(seed_fp(7));
+  for (int it = 0; it < iters; it++) x = wmul_bp(x, y);
+  out[threadIdx.x] = x;
+}
+// an F2 product chain (wf_mul: two half swaps + one wdot2 per half), with the permlane and the ds_bpermute swaps
+__global__ void __launch_bounds__(64) k_wfmul(uint32_t* out, int iters) {
+  const WKG K = wkg_init();
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32)), y = w_from_fp(seed_fp(7 + threadIdx.x / 32));
+  for (int it = 0; it < iters; it++) x = wf_mul(K.kneg, x, y);
+  out[threadIdx.x] = x;
+}
+__global__ void __launch_bounds__(64) k_wfmul_bp(uint32_t* out, int iters) {
+  const WKG K = wkg_init();
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32)), y = w_from_fp(seed_fp(7 + threadIdx.x / 32));
+  for (int it = 0; it < iters; it++) {
+    const bool h = whalf() != 0;
+    const uint32_t sa = wswap_bp(x), sb = wswap_bp(y);
+    const uint32_t nb1 = wnorm(K.kneg - sb);
+    uint64_t a = 0;
+    wmac(a, h ? sa : x, y);
+    wmac(a, h ? x : sa, h ? sb : nb1);
+    x = wredc_bp(a);
+  }
+  out[threadIdx.x] = x;
+}
+// instruction-cache pressure: the same chain with 64 products unrolled (~100 KB of straight-line code, past the
+// instruction cache) against the rolled loop (k_wmul)
+__global__ void __launch_bounds__(64) k_wmul_unr(uint32_t* out, int iters) {
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32)), y = w_from_fp(seed_fp(7));
+  for (int it = 0; it < iters; it += 64) {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) x = wmul(x, y);
+  }
+  out[threadIdx.x] = x;
+}
+// the square-root exponentiation of the SSWU map as compiled in k_h2c_wide (fully unrolled: the exponent is a
+// compile-time constant) and as a rolled loop over the exponent bits
+__global__ void __launch_bounds__(64) k_wpow(uint32_t* out, int iters) {
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32));
+  for (int it = 0; it < iters; ++it) x = wpow(x, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+  out[threadIdx.x] = x;
+}
+__device__ __noinline__ uint32_t wpow_rolled(uint32_t a, const uint32_t* e, int nbits) {
+  const uint32_t a2 = wsqr(a);
+  const uint32_t t1 = a, t3 = wmul(t1, a2), t5 = wmul(t3, a2), t7 = wmul(t5, a2);
+  uint32_t r = t1;
+  bool started = false;
+  int i = nbits - 1;
+#pragma nounroll
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      r = wsqr(r);
+      --i;
+      continue;
+    }
+    int j = i - 2 < 0 ? 0 : i - 2;
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) ++j;
+    uint32_t w = 0;
+#pragma nounroll
+    for (int k = i; k >= j; --k) w = (w << 1) | ((e[k >> 5] >> (k & 31)) & 1u);
+    const uint32_t m = w == 1u ? t1 : (w == 3u ? t3 : (w == 5u ? t5 : t7));
+    if (!started) {
+      r = m;
+      started = true;
+    } else {
+#pragma nounroll
+      for (int k = i; k >= j; --k) r = wsqr(r);
+      r = wmul(r, m);
+    }
+    i = j - 1;
+  }
+  return r;
+}
+__global__ void __launch_bounds__(64) k_wpow_rolled(const uint32_t* e, uint32_t* out, int iters) {
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32));
+  for (int it = 0; it < iters; ++it) x = wpow_rolled(x, e, EXP_SQRT_M3_BITS);
+  out[threadIdx.x] = x;
+  const uint32_t y = wpow(w_from_fp(seed_fp(1 + threadIdx.x / 32)), EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+  const uint32_t z = wpow_rolled(w_from_fp(seed_fp(1 + threadIdx.x / 32)), e, EXP_SQRT_M3_BITS);
+  if (threadIdx.x == 0) out[101] = !fp_eq(w_to_fp(y), w_to_fp(z));
+}
+// the lane-form inversion (bls_fp_inv.h, safegcd) of a wave-uniform value as the wide kernels call it: operand
+// read out of the digits with readlane (SGPRs: the compiler runs it as scalar code), and the same operand moved
+// into VGPRs first (identity DPP per limb: vector code)
+__device__ __forceinline__ Fp fp_vgpr(const Fp& a) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], 0xE4, 0xF, 0xF, false);
+  return r;
+}
+__global__ void __launch_bounds__(64) k_inv_s(uint32_t* out, int iters) {
+  uint32_t x = w_from_fp(seed_fp(5));
+  for (int it = 0; it < iters; ++it) x = w_from_fp(fp_inv_sg_i(w_to_fp(x)));
+  out[threadIdx.x] = x;
+}
+__global__ void __launch_bounds__(64) k_inv_v(uint32_t* out, int iters) {
+  uint32_t x = w_from_fp(seed_fp(5));
+  for (int it = 0; it < iters; ++it) x = w_from_fp(fp_inv_sg_i(fp_vgpr(w_to_fp(x))));
+  out[threadIdx.x] = x;
+}
+// correctness of the new forms against the old on the same chain (0 = equal)
+__global__ void __launch_bounds__(64) k_check(uint32_t* out, int iters) {
+  const WKG K = wkg_init();
+  uint32_t x = w_from_fp(seed_fp(1 + threadIdx.x / 32)), y = w_from_fp(seed_fp(7 + threadIdx.x / 32));
+  uint32_t xo = x;
+  int bad = 0;
+  for (int it = 0; it < iters; it++) {
+    x = wmul(x, y);
+    xo = wmul_bp(xo, y);
+    bad |= !fp_eq(w_to_fp(x), w_to_fp(xo));
+    bad |= !fp_eq(w_to_fp(wswap(x)), w_to_fp(wswap_bp(xo))) ? 2 : 0;
+  }
+  if (threadIdx.x == 0) out[100] = bad;
+}
 __device__ __forceinline__ uint32_t wmul_v1(uint32_t x, uint32_t y) {
   uint64_t a0 = 0, a1 = 0;
   wmac2(a0, a1, x, y);
@@ -124,6 +280,45 @@ __global__ void __launch_bounds__(64) k_fq(uint32_t* out, int iters) {
   out[threadIdx.x] = x.d[0] ^ x.d[13];
 }
 
+// k_h2c_wide (bls_wide.hip) on one 32-byte message with wall-clock stamps (100 MHz) between its stages
+__global__ void __launch_bounds__(64) k_h2c_stages(const uint8_t* msg, uint64_t* ts, uint32_t* out) {
+  uint64_t t[10];
+  t[0] = wall_clock64();
+  const WKG K = wkg_init();
+  Fp2 u[2];
+  hash_to_field_fp2_m32<true>(u, msg);
+  t[1] = wall_clock64();
+  const bool hi = whalf() != 0;
+  const Fp2 uh{fp_select(hi, u[1].c0, u[0].c0), fp_select(hi, u[1].c1, u[0].c1)};
+  W2 x, y;
+  bool rare = false, izero = false, exc = false;
+  sswu_w(K, uh, x, y, rare);
+  t[2] = wall_clock64();
+  const J2W P = iso_w(K, x, y, izero);
+  const J2W Po{w2swap(P.x), w2swap(P.y), w2swap(P.z)};
+  const J2F Q = j2f_of_j2w(j2w_add(K, P, Po, exc));
+  t[3] = wall_clock64();
+  const uint32_t cx = wf_from_fp2(PSI_CX), cy = wf_from_fp2(PSI_CY);
+  const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
+  const J2F M = j2f_mul_xabs(K, Q, exc);
+  t[4] = wall_clock64();
+  const J2F npq = j2f_neg(K, j2f_psi(K, Q, cx, cy));
+  const J2F Ap = j2f_add(K, M, npq, exc);
+  J2F C = j2f_add(K, j2f_psi2(j2f_dbl(K, Q), c2x, c2y), npq, exc);
+  C = j2f_add(K, C, M, exc);
+  C = j2f_add(K, C, j2f_neg(K, Q), exc);
+  t[5] = wall_clock64();
+  const J2F M2 = j2f_mul_xabs(K, Ap, exc);
+  t[6] = wall_clock64();
+  const J2F Hj = j2f_add(K, C, M2, exc);
+  const G2A h = j2f_to_aff(K, Hj);
+  t[7] = wall_clock64();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 8; ++k) ts[k] = t[k];
+    out[0] = h.x.c0.l[0] ^ (rare | izero | exc);
+  }
+}
+
 template <class K>
 static float run(K k, uint32_t* d, int iters) {
   hipEvent_t a, b;
@@ -149,14 +344,63 @@ int main() {
   struct {
     const char* name;
     float ms;
-  } r[] = {{"wmul (shipped)", run(k_wmul, d, N)},
-           {"wmul v1 (two accumulators)", run(k_wmul_v1, d, N)},
-           {"wmul x2 (two chains, per iter)", run(k_wmul_x2, d, N)},
-           {"wdot2", run(k_wdot2, d, N)},
-           {"wmac walk only", run(k_wmac, d, N)},
-           {"wredc only", run(k_wredc, d, N)},
-           {"fq_mul (lane form, one wave)", run(k_fq, d, N)}};
+    int n;
+  } r[] = {{"wmul (permlane moves)", run(k_wmul, d, N), N},
+           {"wmul (ds_bpermute, round 4)", run(k_wmul_bp, d, N), N},
+           {"wf_mul (permlane)", run(k_wfmul, d, N), N},
+           {"wf_mul (ds_bpermute, round 4)", run(k_wfmul_bp, d, N), N},
+           {"wmul 64x unrolled chain", run(k_wmul_unr, d, N), N},
+           {"wmul v1 (two accumulators)", run(k_wmul_v1, d, N), N},
+           {"wmul x2 (two chains, per iter)", run(k_wmul_x2, d, N), N},
+           {"wdot2", run(k_wdot2, d, N), N},
+           {"fp_inv_sg_i, SGPR operand", run(k_inv_s, d, 200), 200},
+           {"fp_inv_sg_i, VGPR operand", run(k_inv_v, d, 200), 200},
+           {"wmac walk only", run(k_wmac, d, N), N},
+           {"wredc only", run(k_wredc, d, N), N},
+           {"fq_mul (lane form, one wave)", run(k_fq, d, N), N}};
   printf("clock %.3f GHz (attribute), %d dependent products per chain, one wave\n", ghz, N);
-  for (auto& x : r) printf("%-32s %8.1f ns/product  %7.0f cycles\n", x.name, x.ms * 1e6 / N, x.ms * 1e6 / N * ghz);
+  for (auto& x : r) printf("%-32s %8.1f ns/op  %7.0f cycles\n", x.name, x.ms * 1e6 / x.n, x.ms * 1e6 / x.n * ghz);
+  {
+    uint32_t bad = 99;
+    hipLaunchKernelGGL(k_check, dim3(1), dim3(64), 0, 0, d, 200);
+    CK(hipMemcpy(&bad, d + 100, 4, hipMemcpyDeviceToHost));
+    printf("permlane forms vs ds_bpermute forms over 200 products: %s (%u)\n", bad ? "MISMATCH" : "equal", bad);
+  }
+  {  // one exponentiation each way (us)
+    uint32_t* de;
+    CK(hipMalloc(&de, 64));
+    CK(hipMemcpy(de, EXP_SQRT_M3, sizeof(EXP_SQRT_M3), hipMemcpyHostToDevice));
+    const float a = run(k_wpow, d, 20);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_wpow_rolled, dim3(1), dim3(64), 0, 0, de, d, 2);
+    hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(k_wpow_rolled, dim3(1), dim3(64), 0, 0, de, d, 20);
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float b = 0;
+    hipEventElapsedTime(&b, e0, e1);
+    uint32_t bad = 9;
+    CK(hipMemcpy(&bad, d + 101, 4, hipMemcpyDeviceToHost));
+    printf("wpow (unrolled, as shipped) %.1f us; rolled loop %.1f us (per exponentiation, %s)\n", a * 1e3 / 20,
+           b * 1e3 / 20, bad ? "MISMATCH" : "same value");
+  }
+  // stage times of the per-call hash_to_G2
+  uint8_t* dm;
+  uint64_t* dts;
+  CK(hipMalloc(&dm, 32));
+  CK(hipMalloc(&dts, 8 * 8));
+  CK(hipMemset(dm, 7, 32));
+  const char* st[7] = {"hash_to_field", "sswu (u0 | u1)", "iso + P0 + P1", "M = [|x|] Q", "psi terms, C", "M2 = [|x|] A'",
+                       "H, affine"};
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(k_h2c_stages, dim3(1), dim3(64), 0, 0, dm, dts, d);
+    CK(hipDeviceSynchronize());
+  }
+  uint64_t hts[8];
+  CK(hipMemcpy(hts, dts, sizeof(hts), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 7; ++k) printf("h2c stage %-16s %8.1f us\n", st[k], (hts[k + 1] - hts[k]) / 100.0);
+  printf("h2c total %.1f us\n", (hts[7] - hts[0]) / 100.0);
   return 0;
 }
