@@ -97,6 +97,9 @@ struct bls_ctx {
   // reservation of (private segment x device wave slots), so they run on two
   // queues instead of on every job's (see k_h2c_fallback).
   hipStream_t fb_stream = nullptr, fe_stream = nullptr;
+  // the per-call API's signature branch (verify_percall, AggregateVerify) beside the hash on stream2 and the keys
+  // on stream1 when job 0 has two streams: one more stream, used by no batch
+  hipStream_t pc_stream = nullptr;
   // registry (HBM resident): RegKey records of 96 B of affine (x, y) padded to 128 B and 128-B aligned (one
   // cache line per random read), validity in x's top bit; 128 MiB per 2^20 keys, 256 MiB for 2^21
   RegKey* reg = nullptr;
@@ -434,6 +437,7 @@ int bls_ctx_create(int device, bls_ctx** out) {
   const char* fev = getenv("BLS_FE_STREAM");
   const bool fe_job = !(fev && !strcmp(fev, "ctx"));
   if (hipStreamCreateWithFlags(&c->fb_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->pc_stream, hipStreamNonBlocking) != hipSuccess ||
       (!fe_job && hipStreamCreateWithPriority(&c->fe_stream, hipStreamNonBlocking, prio_hi) != hipSuccess)) {
     bls_ctx_destroy(c);
     return BLS_E_DEVICE;
@@ -447,7 +451,7 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (Job& J : ctx->jobs) job_destroy(J);
-  for (hipStream_t s : {ctx->fb_stream, ctx->fe_stream})
+  for (hipStream_t s : {ctx->fb_stream, ctx->fe_stream, ctx->pc_stream})
     if (s) {
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);
@@ -477,10 +481,10 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
 }
 
 // Per-call CoreVerify over n keys (n = 1: Verify, E/utils/bls.py:141-151;
-// n > 1: FastAggregateVerify, :167-177), on the three streams of job 0, in
-// wavefront-cooperative arithmetic:
+// n > 1: FastAggregateVerify, :167-177), on three streams, in wavefront-cooperative arithmetic:
 //   stream2: hash_to_G2(msg) on one wave (k_h2c_wide)
-//   stream3: signature decode + G2 subgroup check (k_sig_validate_wide)
+//   stream3 (job 0's third stream, or the context's per-call stream when job 0 has two): signature decode + G2
+//            subgroup check (k_sig_validate_wide)
 //   stream1: KeyValidate of every key (+ their sum), then -- after both
 //            branches -- the Miller loops of (apk, H) and (-G1, sigma) fused on
 //            ONE k_miller_wide workgroup, the six-wave final exponentiation
@@ -528,9 +532,9 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   if (msg_len) memcpy(ctx->pc_stage + 48 * n + 96, msg, msg_len);
   memcpy(ctx->pc_stage + offs_at, offs, sizeof offs);
   CK(h2d(ctx, d_in, ctx->pc_stage, total));
-  // a two-stream job 0 (stream3 aliases stream2): the signature check runs on stream1 ahead of the keys, beside
-  // the hash, instead of behind it
-  const hipStream_t ss = st3 == st2 ? st : st3;
+  // a two-stream job 0 (stream3 aliases stream2): the signature check on the context's per-call stream, beside
+  // the hash and the keys (on stream1 ahead of the keys it made stream1 as long as the hash: 0.8 + 0.7 ms)
+  const hipStream_t ss = st3 != st2 ? st3 : ctx->pc_stream;
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   if (ss != st) HIPCK(hipStreamWaitEvent(ss, J.ev_fork, 0));
@@ -612,7 +616,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   CK(h2d(ctx, d_sig, sig96, 96));
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
-  const hipStream_t ss = st3 == st2 ? st : st3;  // two-stream job 0: the signature check on stream1 (verify_percall)
+  const hipStream_t ss = st3 != st2 ? st3 : ctx->pc_stream;  // two-stream job 0: the per-call stream (verify_percall)
   HIPCK(hipEventRecord(J.ev_fork, st));
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   if (ss != st) HIPCK(hipStreamWaitEvent(ss, J.ev_fork, 0));

@@ -61,8 +61,29 @@ struct SgTrans {
   int64_t u, v, q, r;
 };
 
-// 59 hddivsteps on the low 64 bits of f (odd) and g; t scaled by 2^62 (starts at 8 = 2^3, 59 doublings)
+// a wave-uniform 64-bit value as a scalar (two readfirstlane into SGPRs) on the device
+BLS_HD uint64_t sg_uniform(uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+#else
+  return v;
+#endif
+}
+
+// 59 hddivsteps on the low 64 bits of f (odd) and g; t scaled by 2^62 (starts at 8 = 2^3, 59 doublings).
+// UNIFORM: the value being inverted is the same on every lane (the per-call kernels invert one norm per wave):
+// the step inputs go through SGPRs, so the 59 steps -- 64-bit adds, masks and shifts only, no products -- compile
+// to SALU code, one operation per cycle, instead of VALU code at 4-8 cycles per instruction for one 64-lane wave
+// (tools/microbench/widerate.hip: 126 us per inversion in VALU form).
+template <bool UNIFORM = false>
 BLS_HD int64_t sg_divsteps_59(int64_t zeta, uint64_t f0, uint64_t g0, SgTrans& t) {
+  if (UNIFORM) {
+    zeta = (int64_t)sg_uniform((uint64_t)zeta);
+    f0 = sg_uniform(f0);
+    g0 = sg_uniform(g0);
+  }
   uint64_t u = 8, v = 0, q = 0, r = 8, f = f0, g = g0;
 #pragma unroll 1
   for (int i = 3; i < 62; ++i) {
@@ -208,6 +229,7 @@ BLS_HD Fp sg_to_fp(const S62& x) {  // x in [0, p)
 
 // Plain modular inverse of the integer a (canonical, < p); 0 -> 0.  Inline form for the lane kernels (an
 // out-of-line call gives the kernel a private segment); fp_inv_plain_sg is the out-of-line one.
+template <bool UNIFORM = false>
 BLS_HD Fp fp_inv_plain_sg_i(const Fp& a) {
   S62 f{}, g = sg_from_fp(a), d{}, e{};
 #pragma unroll
@@ -217,8 +239,8 @@ BLS_HD Fp fp_inv_plain_sg_i(const Fp& a) {
 #pragma unroll 1
   for (int it = 0; it < 15; it++) {
     SgTrans t;
-    zeta = sg_divsteps_59(zeta, (uint64_t)f.v[0] | ((uint64_t)f.v[1] << 62), (uint64_t)g.v[0] | ((uint64_t)g.v[1] << 62),
-                          t);
+    zeta = sg_divsteps_59<UNIFORM>(zeta, (uint64_t)f.v[0] | ((uint64_t)f.v[1] << 62),
+                                   (uint64_t)g.v[0] | ((uint64_t)g.v[1] << 62), t);
     sg_update_de(d, e, t);
     sg_update_fg(f, g, t);
   }
@@ -231,7 +253,8 @@ BLS_HDNI Fp fp_inv_plain_sg(const Fp& a) { return fp_inv_plain_sg_i(a); }
 
 // Montgomery-form inverse, as fp_inv: (a R)^-1 R^3 / R = a^-1 R
 BLS_HD Fp fp_inv_sg(const Fp& a) { return fp_mul(fp_inv_plain_sg(a), FP_R3); }
-BLS_HD Fp fp_inv_sg_i(const Fp& a) { return fp_mul_i(fp_inv_plain_sg_i(a), FP_R3); }
+template <bool UNIFORM = false>
+BLS_HD Fp fp_inv_sg_i(const Fp& a) { return fp_mul_i(fp_inv_plain_sg_i<UNIFORM>(a), FP_R3); }
 // the general Montgomery-form inverse (0 -> 0).  It replaced a bit-serial binary extended Euclid whose
 // data-dependent branches diverged across the lanes of the batch kernels (~170k VALU instructions per inverse).
 BLS_HDNI Fp fp_inv(const Fp& a) { return fp_mul(fp_inv_plain_sg_i(a), FP_R3); }

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64) k_h2c_wide(size_t B, const uint8_t* msgs, 
   if (offs)
     hash_to_field_fp2(u, msgs + offs[i], (uint32_t)(offs[i + 1] - offs[i]), DST_POP_WIDE, 43);
   else
-    hash_to_field_fp2_m32(u, msgs + 32 * i);
+    hash_to_field_fp2_m32<true>(u, msgs + 32 * i);
   const bool hi = whalf() != 0;
   const Fp2 uh{fp_select(hi, u[1].c0, u[0].c0), fp_select(hi, u[1].c1, u[0].c1)};
   W2 x, y;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void dbg_put(Fp* out, int k, const Fp& v) {
 __global__ void __launch_bounds__(64) k_h2c_wide_dbg(const uint8_t* msg32, Fp* out) {
   const WKG K = wkg_init();
   Fp2 u[2];
-  hash_to_field_fp2_m32(u, msg32);
+  hash_to_field_fp2_m32<true>(u, msg32);
   const bool hi = whalf() != 0;
   const Fp2 uh{fp_select(hi, u[1].c0, u[0].c0), fp_select(hi, u[1].c1, u[0].c1)};
   W2 x, y;

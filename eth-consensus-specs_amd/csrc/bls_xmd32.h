@@ -190,13 +190,25 @@ BLS_HD Fp fp_from_be64w_mod(const uint32_t w[16]) {
   return fp_add(fp_mul_i(lo, FP_R2), fp_mul_i(hi, FP_2P384_R2));
 }
 
-// u[0], u[1] = hash_to_field(msg, 2) for a 32-byte message under the POP DST (RFC 9380 §5.2, m = 2, L = 64)
+// a wave-uniform word kept in a VGPR: on the device an identity DPP move hides its uniformity from the
+// compiler, so the compressions of one message run as VALU code (v_alignbit rotates, v_xor3, v_bitop3, v_add3)
+// instead of scalar code that sends every rotate through a VALU v_alignbit and a v_readfirstlane back
+BLS_HD uint32_t xmd_vector(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xE4, 0xF, 0xF, false);  // quad_perm [0,1,2,3]
+#else
+  return v;
+#endif
+}
+
+template <bool UNIFORM = false>
 BLS_HD void hash_to_field_fp2_m32(Fp2 u[2], const uint8_t* msg32) {
   uint32_t blk[16], st[8], b0[8], bi[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const uint8_t* q = msg32 + 4 * j;
     blk[j] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+    if (UNIFORM) blk[j] = xmd_vector(blk[j]);
   }
 #pragma unroll
   for (int j = 8; j < 16; j++) blk[j] = xmd32::B0_BLK2.w[j];
