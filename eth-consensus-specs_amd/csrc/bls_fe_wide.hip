@@ -125,7 +125,7 @@ struct FeWide {
       const uint32_t d = wredc(acc);
       const uint32_t sq = wsqr(d);
       const Fp nl = w_to_fp(wadd(sq, wswap(sq)));  // norm(d) in both halves
-      const uint32_t ni = w_from_fp(fp_inv_sg_i<true>(nl));  // wave-uniform: scalar divsteps
+      const uint32_t ni = w_from_fp(fp_inv_sg_i(nl));
       B[(4 * 6 + 0) * 64 + lane] = wmul(wf_conj(K.k1, d), ni);
     }
     __syncthreads();

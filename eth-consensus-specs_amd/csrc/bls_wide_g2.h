@@ -209,7 +209,7 @@ __device__ __forceinline__ G2A j2w_to_aff(const WKG& K, const J2W& p) {
   const uint32_t nz = wadd(wsqr(p.z.c0), wsqr(p.z.c1));  // norm(Z)
   const Fp nl = w_to_fp(nz);
   G2A r{fp2_zero(), fp2_zero(), true};
-  const uint32_t ni = w_from_fp(fp_inv_sg_i<true>(nl));  // nl is the same on every lane: scalar divsteps
+  const uint32_t ni = w_from_fp(fp_inv_sg_i(nl));
   const W2 zi{wmul(p.z.c0, ni), wneg(wk_of(K), wmul(p.z.c1, ni))};
   const W2 zi2 = w2mulk(K, zi, zi);
   const W2 zi3 = w2mulk(K, zi2, zi);
@@ -300,7 +300,7 @@ __device__ __forceinline__ G2A j2f_to_aff(const WKG& K, const J2F& p) {
   const uint32_t nz = wadd(sq, wswap(sq));  // norm(Z) in both halves
   const Fp nl = w_to_fp(nz);
   G2A r{fp2_zero(), fp2_zero(), true};
-  const uint32_t ni = w_from_fp(fp_inv_sg_i<true>(nl));  // nl is the same on every lane: scalar divsteps
+  const uint32_t ni = w_from_fp(fp_inv_sg_i(nl));
   const uint32_t zi = wmul(wf_conj(K.k2048_2, p.z), ni);
   const uint32_t zi2 = wf_mul(K.kneg, zi, zi);
   const uint32_t zi3 = wf_mul(K.kneg, zi2, zi);

@@ -414,7 +414,7 @@ def test_fe_lane_schedule():
 
 
 def test_fp_inv_safegcd():
-    """fp_inv_sg (bls_fp_inv.h, Bernstein-Yang divsteps, 15 x 59 steps) against pow(x, -1, p): random values,
+    """fp_inv_sg (bls_fp_inv.h, Bernstein-Yang divsteps, 30 x 30 steps on 30-bit limbs) against pow(x, -1, p): random values,
     the edges 0, 1, 2, p - 1, p - 2 and values with long runs of zero / one bits."""
     vals = [0, 1, 2, O.P - 1, O.P - 2, (1 << 380) - 1, 1 << 380, (O.P - 1) // 2, 3 << 300]
     vals += [rng.randrange(O.P) for _ in range(300)]

@@ -214,14 +214,6 @@ __global__ void __launch_bounds__(64) k_inv_v(uint32_t* out, int iters) {
   for (int it = 0; it < iters; ++it) x = w_from_fp(fp_inv_sg_i(fp_vgpr(w_to_fp(x))));
   out[threadIdx.x] = x;
 }
-__global__ void __launch_bounds__(64) k_inv_u(uint32_t* out, int iters) {
-  uint32_t x = w_from_fp(seed_fp(5));
-  for (int it = 0; it < iters; ++it) x = w_from_fp(fp_inv_sg_i<true>(w_to_fp(x)));
-  out[threadIdx.x] = x;
-  // the uniform form against the vector form on the same operand
-  const Fp a = w_to_fp(w_from_fp(seed_fp(9)));
-  if (threadIdx.x == 0) out[102] = !fp_eq(fp_inv_sg_i<true>(a), fp_inv_sg_i(fp_vgpr(a)));
-}
 // correctness of the new forms against the old on the same chain (0 = equal)
 __global__ void __launch_bounds__(64) k_check(uint32_t* out, int iters) {
   const WKG K = wkg_init();
@@ -363,7 +355,6 @@ int main() {
            {"wdot2", run(k_wdot2, d, N), N},
            {"fp_inv_sg_i, SGPR operand", run(k_inv_s, d, 200), 200},
            {"fp_inv_sg_i, VGPR operand", run(k_inv_v, d, 200), 200},
-           {"fp_inv_sg_i<true> (SALU steps)", run(k_inv_u, d, 200), 200},
            {"wmac walk only", run(k_wmac, d, N), N},
            {"wredc only", run(k_wredc, d, N), N},
            {"fq_mul (lane form, one wave)", run(k_fq, d, N), N}};
@@ -374,8 +365,6 @@ int main() {
     hipLaunchKernelGGL(k_check, dim3(1), dim3(64), 0, 0, d, 200);
     CK(hipMemcpy(&bad, d + 100, 4, hipMemcpyDeviceToHost));
     printf("permlane forms vs ds_bpermute forms over 200 products: %s (%u)\n", bad ? "MISMATCH" : "equal", bad);
-    CK(hipMemcpy(&bad, d + 102, 4, hipMemcpyDeviceToHost));
-    printf("uniform (scalar) inversion vs vector inversion: %s\n", bad ? "MISMATCH" : "equal");
   }
   {  // one exponentiation each way (us)
     uint32_t* de;
