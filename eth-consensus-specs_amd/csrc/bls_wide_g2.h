@@ -282,6 +282,53 @@ __device__ __forceinline__ J2F j2f_mul_xabs(const WKG& K, const J2F& p, bool& ex
   }
   return m;
 }
+// The same doubling on THREE waves of one workgroup (the per-call hash's cofactor chains, k_h2c_wide): its seven
+// F2 products have dependency depth 3 -- {A = X^2, B = Y^2, YZ = Y Z}, {C = B^2, XB2 = (X + B)^2, EE = (3A)^2},
+// {E (D - X3)} -- so wave w forms product w of each of the first two levels, the waves exchange them through LDS
+// (one barrier per level), and every wave forms the last product itself.  Each wave ends with the whole point,
+// the same values as j2f_dbl's.  x3: 6 x 64 words of LDS; w: this wave's index (0, 1, 2), uniform per wave.
+__device__ __forceinline__ J2F j2f_dbl3(const WKG& K, const J2F& p, uint32_t* x3, int w) {
+  const uint32_t ks = K.k2048_2, kn = K.kneg;
+  const int l = wlane();
+  uint32_t m1;
+  if (w == 0)
+    m1 = wf_sqr(ks, p.x);
+  else if (w == 1)
+    m1 = wf_sqr(ks, p.y);
+  else
+    m1 = wf_mul(kn, p.y, p.z);
+  x3[w * 64 + l] = m1;
+  __syncthreads();
+  const uint32_t A = x3[l], Bq = x3[64 + l], YZ = x3[128 + l];
+  const uint32_t E = wmuls<3>(A);
+  uint32_t m2;
+  if (w == 0)
+    m2 = wf_sqr(ks, Bq);
+  else if (w == 1)
+    m2 = wf_sqr(ks, wadd(p.x, Bq));
+  else
+    m2 = wf_sqr(ks, E);
+  x3[(3 + w) * 64 + l] = m2;
+  __syncthreads();
+  const uint32_t C = x3[192 + l], XB2 = x3[256 + l], EE = x3[320 + l];
+  const uint32_t D = wmuls<2>(wsubk(K.k2, XB2, wadd(A, C)));
+  J2F r;
+  r.x = wsubk(K.k1024, EE, wmuls<2>(D));
+  const uint32_t DX = wsubk(K.k2048_2, D, r.x);
+  r.y = wsubk(K.k1, wf_mul(kn, E, DX), wmuls<8>(C));
+  r.z = wmuls<2>(YZ);
+  return r;
+}
+// [|x|] p with the doublings on three waves (the additions on every wave)
+__device__ __forceinline__ J2F j2f_mul_xabs3(const WKG& K, const J2F& p, bool& exc, uint32_t* x3, int w) {
+  J2F m = p;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    m = j2f_dbl3(K, m, x3, w);
+    if ((X_ABS >> b) & 1ull) m = j2f_add(K, m, p, exc);
+  }
+  return m;
+}
 __device__ __forceinline__ J2F j2f_neg(const WKG& K, const J2F& p) {
   return J2F{p.x, wsubk(K.k1, 0u, wmul(p.y, K.one)), p.z};
 }

@@ -280,8 +280,10 @@ __global__ void __launch_bounds__(64) k_fq(uint32_t* out, int iters) {
   out[threadIdx.x] = x.d[0] ^ x.d[13];
 }
 
-// k_h2c_wide (bls_wide.hip) on one 32-byte message with wall-clock stamps (100 MHz) between its stages
-__global__ void __launch_bounds__(64) k_h2c_stages(const uint8_t* msg, uint64_t* ts, uint32_t* out) {
+// k_h2c_wide (bls_wide.hip, three waves) on one 32-byte message with wall-clock stamps (100 MHz) between its stages
+__global__ void __launch_bounds__(192) k_h2c_stages(const uint8_t* msg, uint64_t* ts, uint32_t* out) {
+  __shared__ uint32_t x3[6 * 64];
+  const int w = (int)(threadIdx.x >> 6);
   uint64_t t[10];
   t[0] = wall_clock64();
   const WKG K = wkg_init();
@@ -300,7 +302,7 @@ __global__ void __launch_bounds__(64) k_h2c_stages(const uint8_t* msg, uint64_t*
   t[3] = wall_clock64();
   const uint32_t cx = wf_from_fp2(PSI_CX), cy = wf_from_fp2(PSI_CY);
   const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
-  const J2F M = j2f_mul_xabs(K, Q, exc);
+  const J2F M = j2f_mul_xabs3(K, Q, exc, x3, w);
   t[4] = wall_clock64();
   const J2F npq = j2f_neg(K, j2f_psi(K, Q, cx, cy));
   const J2F Ap = j2f_add(K, M, npq, exc);
@@ -308,7 +310,7 @@ __global__ void __launch_bounds__(64) k_h2c_stages(const uint8_t* msg, uint64_t*
   C = j2f_add(K, C, M, exc);
   C = j2f_add(K, C, j2f_neg(K, Q), exc);
   t[5] = wall_clock64();
-  const J2F M2 = j2f_mul_xabs(K, Ap, exc);
+  const J2F M2 = j2f_mul_xabs3(K, Ap, exc, x3, w);
   t[6] = wall_clock64();
   const J2F Hj = j2f_add(K, C, M2, exc);
   const G2A h = j2f_to_aff(K, Hj);
@@ -395,7 +397,7 @@ int main() {
   const char* st[7] = {"hash_to_field", "sswu (u0 | u1)", "iso + P0 + P1", "M = [|x|] Q", "psi terms, C", "M2 = [|x|] A'",
                        "H, affine"};
   for (int rep = 0; rep < 3; ++rep) {
-    hipLaunchKernelGGL(k_h2c_stages, dim3(1), dim3(64), 0, 0, dm, dts, d);
+    hipLaunchKernelGGL(k_h2c_stages, dim3(1), dim3(192), 0, 0, dm, dts, d);
     CK(hipDeviceSynchronize());
   }
   uint64_t hts[8];
