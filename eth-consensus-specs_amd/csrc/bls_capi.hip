@@ -1201,7 +1201,9 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   // launch under-fills the chip and the chain latency is what counts, so one pair per f (a step is a squaring
   // and ONE line: ~37 % shorter chains for ~24 % more products)
   static const int acc_g = getenv("BLS_ACC_G") ? atoi(getenv("BLS_ACC_G")) : 2;  // pairs per f of full batches
-  const int mg = B >= ACC_SHARED_MIN ? (acc_g == 4 ? 4 : (acc_g == 1 ? 1 : 2)) : 1;
+  static const size_t shared_min = getenv("BLS_ACC_SHARED_MIN") ? (size_t)atol(getenv("BLS_ACC_SHARED_MIN"))
+                                                                : ACC_SHARED_MIN;
+  const int mg = B >= shared_min ? (acc_g == 4 ? 4 : (acc_g == 1 ? 1 : 2)) : 1;
   J.fav_mg = mg;
   if (fused)
     PROF(5, launch_miller_fused(st, rP, H, status, NP, f, mg));
