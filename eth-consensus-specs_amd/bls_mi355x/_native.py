@@ -10,7 +10,7 @@ import ctypes
 import os
 import threading
 
-HW_QUEUES = 24  # 10 FAV jobs x 2 streams + the fallback stream share them with the default/copy streams
+HW_QUEUES = 24  # 10 FAV jobs x 2 streams + the fallback and per-call streams share them with the default/copy streams
 
 
 def hw_queue_policy() -> None:

@@ -4,10 +4,11 @@
 // nonzero digit d are counting-sorted into 8 x 255 buckets (atomic histogram,
 // one block-wide prefix scan, atomic scatter).  Seven launches:
 //   k_msm_count, k_msm_scan, k_msm_scatter   the sort
-//   k_msm_bucketc   each bucket's points summed in MSM_C = 8 strided chunks,
-//                   one lane pair per chunk (~5 mixed additions each; 16,384
-//                   chunks = 512 waves, the point loads one step ahead), the
-//                   chunks then folded into the bucket sum B_{w,d} in LDS
+//   k_msm_bucketc   each bucket's points summed in C strided chunks (C = 8 for
+//                   a C2 batch: one lane pair per chunk, ~5 mixed additions
+//                   each, 16,384 chunks = 512 waves, the point loads one step
+//                   ahead; fewer for smaller batches, msm_chunks), the chunks
+//                   then folded into the bucket sum B_{w,d} in LDS
 //   k_msm_usum      U_b = sum_{d : bit k of d} B_{w,d}  (b = 8w + k): one
 //                   wave per b, 32 lane pairs adding 4 bucket sums each, then a
 //                   5-level LDS tree (a 16-wave wide-arithmetic variant
@@ -86,7 +87,14 @@ __global__ void __launch_bounds__(256) k_msm_scatter(size_t B, const int* status
   if (d) lst[atomicAdd(&cur[w * 256 + d], 1u)] = (uint32_t)i;
 }
 
-constexpr int MSM_C = 8;  // chunks per bucket
+constexpr int MSM_CMAX = 8;  // chunks per bucket, at most (msm_chunks)
+// chunks per bucket for a batch of B items: ~B / 255 points per bucket (8 windows of 255 nonzero digits); enough
+// chunks that a bucket's chain stays short on full batches, few enough that a C3- or C5-size batch is not mostly
+// fold tree and idle lanes (8 chunks of ~1 point each plus a 3-level fold at 2,048 items)
+static int msm_chunks(size_t B) {
+  const size_t per = B / 255;
+  return per >= 32 ? 8 : per >= 12 ? 4 : per >= 4 ? 2 : 1;
+}
 using P2 = PP<Fp2>;
 
 // ----------------------------------------------------------- lane form --
@@ -106,6 +114,7 @@ __device__ __forceinline__ P2 p2_load(const Fp* in) {
 }  // namespace
 
 // chunk c of bucket b (lane pair (b, c)): csum[b C + c] = sum of the bucket's points k = off[b] + c + j C
+template <int MSM_C>
 __global__ void __launch_bounds__(64) k_msm_bucketc(const uint32_t* off, const uint32_t* lst, const G2A* sig,
                                                     Fp* csum) {
   const int t = blockIdx.x * 64 + threadIdx.x;
@@ -127,7 +136,7 @@ __global__ void __launch_bounds__(64) k_msm_bucketc(const uint32_t* off, const u
     li = k + 2 * MSM_C < end ? lst[k + 2 * MSM_C] : 0u;
     R = pp2_add_aff(R, cq.x, cq.y, hi);
   }
-  // the bucket's MSM_C chunk sums (lane pairs 8 b' .. 8 b' + 7 of this wave) folded by a 3-level LDS tree, so the
+  // the bucket's MSM_C chunk sums (lane pairs C b' .. C b' + C - 1 of this wave) folded by a log2(C)-level LDS tree, so the
   // U sums read one point per bucket instead of re-adding its chunks once per set bit of the digit
   __shared__ Fp sm[32 * 6];
   const int lp = threadIdx.x >> 1;  // lane pair in the wave
@@ -186,9 +195,9 @@ __global__ void __launch_bounds__(64) k_msm_upairs(const Fp* U, const G1A* comb,
 }
 
 // Scratch: cnt[MSM_NB] | off[MSM_NB + 1] | cur[MSM_NB] (u32), lst[8 B] (u32);
-// points (packed Fp, 6 per point, in units of Fd slots): chunk sums [MSM_NB * MSM_C] | U [64].
+// points (packed Fp, 6 per point, in units of Fd slots): chunk sums [MSM_NB * MSM_CMAX] | U [64].
 size_t msm_scratch_u32(size_t B) { return (size_t)3 * MSM_NB + 1 + MSM_W * B; }
-size_t msm_scratch_fd() { return ((size_t)(MSM_NB * MSM_C + 64) * 6 * sizeof(Fp) + sizeof(Fd) - 1) / sizeof(Fd); }
+size_t msm_scratch_fd() { return ((size_t)(MSM_NB * MSM_CMAX + 64) * 6 * sizeof(Fp) + sizeof(Fd) - 1) / sizeof(Fd); }
 
 hipError_t launch_msm_upairs(hipStream_t st, size_t B, const int* status, const int* status2, const uint64_t* rsc,
                              const G2A* sig, uint32_t* scr, Fd* pts, const G1A* comb, G1A* P, G2A* Q, int* ok) {
@@ -197,7 +206,7 @@ hipError_t launch_msm_upairs(hipStream_t st, size_t B, const int* status, const 
   uint32_t* cur = off + MSM_NB + 1;
   uint32_t* lst = cur + MSM_NB;
   Fp* csum = reinterpret_cast<Fp*>(pts);
-  Fp* U = csum + (size_t)MSM_NB * MSM_C * 6;
+  Fp* U = csum + (size_t)MSM_NB * MSM_CMAX * 6;
   hipError_t e = hipMemsetAsync(cnt, 0, MSM_NB * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   const unsigned nb = (unsigned)((B * MSM_W + 255) / 256);
@@ -211,7 +220,12 @@ hipError_t launch_msm_upairs(hipStream_t st, size_t B, const int* status, const 
     hipLaunchKernelGGL(k_msm_scatter, dim3(nb), dim3(256), 0, st, B, status, status2, rsc, cur, lst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_msm_bucketc, dim3(2 * MSM_NB * MSM_C / 64), dim3(64), 0, st, off, lst, sig, csum);
+  switch (msm_chunks(B)) {
+    case 8: hipLaunchKernelGGL(k_msm_bucketc<8>, dim3(2 * MSM_NB * 8 / 64), dim3(64), 0, st, off, lst, sig, csum); break;
+    case 4: hipLaunchKernelGGL(k_msm_bucketc<4>, dim3(2 * MSM_NB * 4 / 64), dim3(64), 0, st, off, lst, sig, csum); break;
+    case 2: hipLaunchKernelGGL(k_msm_bucketc<2>, dim3(2 * MSM_NB * 2 / 64), dim3(64), 0, st, off, lst, sig, csum); break;
+    default: hipLaunchKernelGGL(k_msm_bucketc<1>, dim3(2 * MSM_NB / 64), dim3(64), 0, st, off, lst, sig, csum);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_usum, dim3(64), dim3(2 * USUM_PAIRS), 0, st, csum, U);
   if ((e = hipGetLastError()) != hipSuccess) return e;
