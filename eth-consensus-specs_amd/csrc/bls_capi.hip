@@ -807,6 +807,12 @@ int bls_hash_to_g2(bls_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8
 int bls_test_force_h2c_fallback(bls_ctx* ctx, const uint8_t* mask, size_t n) {
   API_ENTER(ctx);
   if (!mask && n) return BLS_E_ARG;
+  // the one hook that changes later calls' routing: refused unless the process opted in (tests/conftest.py)
+  const char* opt = getenv("BLSMI355X_TEST_HOOKS");
+  if (!opt || strcmp(opt, "1") != 0) {
+    ctx->err = "bls_test_force_h2c_fallback needs BLSMI355X_TEST_HOOKS=1";
+    return BLS_E_ARG;
+  }
   HIPCK(hipDeviceSynchronize());
   if (ctx->force_fb) HIPCK(hipFree(ctx->force_fb));
   ctx->force_fb = nullptr;

@@ -406,37 +406,65 @@ __device__ __forceinline__ G1W g1w_add(const WKG& K, const G1W& p, const G1W& q)
   r.z = wadd(wmul(z3, t4), wmul(t0p, t3));
   return r;
 }
-__device__ __forceinline__ G1W g1w_dbl(const WKG& K, const G1W& p) {
-  const uint32_t t0 = wmul(p.y, p.y);
-  const uint32_t t1 = wmul(p.y, p.z);
-  const uint32_t t2 = wmuls<12>(wmul(p.z, p.z));  // 3b Z^2, < 24p
-  const uint32_t u = wmul(p.x, p.y);
+// Complete projective doubling (RCB alg. 9, a = 0, as bls_fq.h's G1 chain) on FOUR waves of one workgroup (the
+// per-call key check, k_key_validate_wide): its eight products have dependency depth 2 -- {Y^2, Y Z, Z^2, X Y}, then {t2 z8, t1 z8, w (t0 + t2), w u} -- so wave w
+// forms product w of each level, the waves exchange them through LDS (one barrier per level), and every wave ends
+// with the whole point.  x4: 8 x 64 words of LDS; w: this wave's index (0 .. 3), uniform per wave.
+__device__ __forceinline__ G1W g1w_dbl4(const WKG& K, const G1W& p, uint32_t* x4, int w) {
+  const int l = wlane();
+  uint32_t m1;
+  if (w == 0)
+    m1 = wmul(p.y, p.y);
+  else if (w == 1)
+    m1 = wmul(p.y, p.z);
+  else if (w == 2)
+    m1 = wmul(p.z, p.z);
+  else
+    m1 = wmul(p.x, p.y);
+  x4[w * 64 + l] = m1;
+  __syncthreads();
+  const uint32_t t0 = x4[l], t1 = x4[64 + l], t2 = wmuls<12>(x4[128 + l]), u = x4[192 + l];
   const uint32_t z8 = wmuls<8>(t0);
-  const uint32_t x3a = wmul(t2, z8);
+  const uint32_t wv = wsubk(K.k2, t0, wmuls<3>(t2));
+  uint32_t m2;
+  if (w == 0)
+    m2 = wmul(t2, z8);
+  else if (w == 1)
+    m2 = wmul(t1, z8);
+  else if (w == 2)
+    m2 = wmul(wv, wadd(t0, t2));
+  else
+    m2 = wmul(wv, u);
+  x4[(4 + w) * 64 + l] = m2;
+  __syncthreads();
   G1W r;
-  r.z = wmul(t1, z8);
-  const uint32_t w = wsubk(K.k2, t0, wmuls<3>(t2));  // t0 - 3 t2 + 128p
-  r.y = wadd(wmul(w, wadd(t0, t2)), x3a);
-  r.x = wmuls<2>(wmul(w, u));
+  r.z = x4[320 + l];
+  r.y = wadd(x4[384 + l], x4[256 + l]);
+  r.x = wmuls<2>(x4[448 + l]);
   return r;
 }
+
+// [|x|] b with the doublings on four waves (the additions on every wave)
 template <bool AFF>
-__device__ __forceinline__ G1W g1w_mul_xabs(const WKG& K, const G1W& b) {
+__device__ __forceinline__ G1W g1w_mul_xabs4(const WKG& K, const G1W& b, uint32_t* x4, int w) {
   G1W m = b;
 #pragma unroll 1
   for (int i = 62; i >= 0; --i) {
-    m = g1w_dbl(K, m);
+    m = g1w_dbl4(K, m, x4, w);
     if ((X_ABS >> i) & 1ull) m = AFF ? g1w_add_aff(K, m, b.x, b.y) : g1w_add(K, m, b);
   }
   return m;
 }
 
 // KeyValidate of keys 2 blockIdx.x + half (k_key_validate semantics; the decode on every lane of the half, the
-// square root and both [|x|] chains in wide arithmetic).  Wave-uniform control flow: the two halves' decode
-// verdicts are combined into selects, not branches.
-__global__ void __launch_bounds__(64) k_key_validate_wide(const uint8_t* pks48, size_t n, G1A* out, int* ok) {
+// square root and both [|x|] chains in wide arithmetic), on a workgroup of four waves doing the same work except
+// the chains' doublings, whose products are spread over the four (g1w_dbl4).  Wave-uniform control flow: the two
+// halves' decode verdicts are combined into selects, not branches.
+__global__ void __launch_bounds__(256) k_key_validate_wide(const uint8_t* pks48, size_t n, G1A* out, int* ok) {
   const size_t base = 2 * (size_t)blockIdx.x;
-  if (base >= n) return;
+  if (base >= n) return;  // (the whole workgroup)
+  __shared__ uint32_t x4[8 * 64];
+  const int wv = (int)(threadIdx.x >> 6);
   const WKG K = wkg_init();
   const WK K1 = wk_of(K);
   const int h = whalf();
@@ -460,7 +488,8 @@ __global__ void __launch_bounds__(64) k_key_validate_wide(const uint8_t* pks48, 
   const uint32_t ny = wmul(wneg(K1, yr), K.one);
   const uint32_t y = flip ? ny : yr;
   const G1W P{xm, y, K.one};
-  const G1W Q = g1w_mul_xabs<false>(K, g1w_mul_xabs<true>(K, P));
+  const G1W Q = g1w_mul_xabs4<false>(K, g1w_mul_xabs4<true>(K, P, x4, wv), x4, wv);
+  if (wv) return;  // waves 1 .. 3: no barrier after the chains
   const bool eq_x = w_eq(K1, wmul(wmul(xm, w_from_fp(FP_BETA)), Q.z), wmul(Q.x, K.one));
   const bool eq_y = w_is_zero(wadd(wmul(y, Q.z), Q.y));
   const bool v = fmt && on && eq_x && eq_y;
@@ -473,7 +502,7 @@ __global__ void __launch_bounds__(64) k_key_validate_wide(const uint8_t* pks48, 
 
 hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_key_validate_wide, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, pks, n, out, ok);
+  hipLaunchKernelGGL(k_key_validate_wide, dim3((unsigned)((n + 1) / 2)), dim3(256), 0, st, pks, n, out, ok);
   return hipGetLastError();
 }
 

@@ -291,6 +291,8 @@ int bls_set_entropy_source(const char* path);
  * bls_test_force_h2c_fallback: items i < n with mask[i] != 0 of every later
  * hash_to_G2 (batch, per-call, AggregateVerify) take the reference-path
  * fallback kernel as if the lane kernels had flagged them; n = 0 clears.
+ * Refused (BLS_E_ARG) unless the environment has BLSMI355X_TEST_HOOKS=1, so a
+ * production process cannot reroute its hashes by accident.
  * bls_test_hash_to_g2_batch: hash_to_G2 (DST POP) of n 32-byte messages through
  * the FAV batch's kernels and fallback routing, compressed into out96. */
 int bls_test_force_h2c_fallback(bls_ctx* ctx, const uint8_t* mask, size_t n);

@@ -4,6 +4,7 @@ batches (C3) and AggregateVerify with many distinct messages (C5), checked
 against verdicts known by construction and the C oracle (oracle/bls_oracle.c).
 Requires an MI355X."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -233,6 +234,12 @@ def test_h2c_fallback_routing_forced(batch, registry):
     msgs = [hashlib.sha256(b"forced-fallback" + j.to_bytes(4, "little")).digest() for j in range(n)]
     forced = {0, 5, 63, 64, 69}
     mask = bytes(1 if j in forced else 0 for j in range(n))
+    # the hook refuses without the process's opt-in (tests/conftest.py sets it)
+    saved = os.environ.pop("BLSMI355X_TEST_HOOKS", None)
+    try:
+        assert ctx.lib.bls_test_force_h2c_fallback(ctx.h, mask, n) == -2  # BLS_E_ARG
+    finally:
+        os.environ["BLSMI355X_TEST_HOOKS"] = saved or "1"
     ctx.check(ctx.lib.bls_test_force_h2c_fallback(ctx.h, mask, n))
     try:
         out = ctypes.create_string_buffer(96 * n)
