@@ -518,6 +518,16 @@ constexpr int MLW_STEPS = 68;  // 63 doublings + 5 additions
 // < 2.0001): doubling in X < 516, Y, Z < 66 -> X3 < 516, Y3, Z3 < 66; addition -> all < 66; lines l0 < 66,
 // l2 and l3 products.  Subtraction constants: 64p for products and small sums, 256p / 512p / 1024p where the
 // subtrahend is a coordinate; the Fp2 products negate with 4096p (kneg), squarings with 2048p.
+struct WaveBar {  // barrier of the first nw waves of the workgroup: cnt counts arrivals, gen is this wave's target
+  int* cnt;
+  int gen, nw;
+  __device__ void sync() {
+    gen += nw;
+    if (wlane() == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+  }
+};
+
 struct LineW {
   uint32_t X, Y, Z, xQ, yQ, nxP, yP;
   __device__ void init(const G1A& P, const G2A& Q, bool live) {
@@ -530,29 +540,42 @@ struct LineW {
     Y = yQ;
     Z = wf_from_fp2(fp2_one());
   }
-  // doubling step: T = 2T, the record (l0, l2, l3) into o[0], o[64], o[128]
-  __device__ void dbl(const WKG& K, uint32_t* o) {
+  // the doubling step on the pair's three line waves (w = 0, 1, 2): dbl's thirteen products in five rounds --
+  // {A = X^2, B = Y^2, ZZ = Z^2}, {(Y + Z)^2, C = B^2, F = E^2}, {(X + B)^2, E X, E ZZ}, {z3 ZZ, E (D - x3),
+  // E ZZ (-x_P)}, then l3 on wave 0 alone -- exchanged through xs (12 x 64 words) with the trio's counter barrier
+  // tb (the f waves never wait on it).  Every wave ends with T = 2T (dbl-2009-l); wave 0 writes the record
+  // (l0, l2, l3) into o[0], o[64], o[128].
+  __device__ void dbl3(const WKG& K, uint32_t* o, uint32_t* xs, int w, WaveBar& tb) {
     const uint32_t kn = K.kneg, ks = K.k2048_2;
-    const uint32_t A = wf_sqr(ks, X), B = wf_sqr(ks, Y), C = wf_sqr(ks, B);
-    const uint32_t XB = wf_sqr(ks, wadd(X, B));
-    const uint32_t D = wmuls<2>(wsubk(K.k1, XB, wadd(A, C)));
+    const int l = wlane();
+    xs[w * 64 + l] = w == 0 ? wf_sqr(ks, X) : (w == 1 ? wf_sqr(ks, Y) : wf_sqr(ks, Z));
+    tb.sync();
+    const uint32_t A = xs[l], B = xs[64 + l], ZZ = xs[128 + l];
     const uint32_t E = wmuls<3>(A);
-    const uint32_t F = wf_sqr(ks, E), ZZ = wf_sqr(ks, Z);
-    const uint32_t l0 = wsubk(K.k1, wf_mul(kn, E, X), wmuls<2>(B));
-    const uint32_t l2 = wmul(wf_mul(kn, E, ZZ), nxP);
-    const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Y, Z)), wadd(B, ZZ));
-    const uint32_t l3 = wmul(wf_mul(kn, z3, ZZ), yP);
+    xs[(3 + w) * 64 + l] = w == 0 ? wf_sqr(ks, wadd(Y, Z)) : (w == 1 ? wf_sqr(ks, B) : wf_sqr(ks, E));
+    tb.sync();
+    const uint32_t YZ2 = xs[192 + l], C = xs[256 + l], F = xs[320 + l];
+    xs[(6 + w) * 64 + l] = w == 0 ? wf_sqr(ks, wadd(X, B)) : (w == 1 ? wf_mul(kn, E, X) : wf_mul(kn, E, ZZ));
+    tb.sync();
+    const uint32_t XB = xs[384 + l], EX = xs[448 + l], EZZ = xs[512 + l];
+    const uint32_t D = wmuls<2>(wsubk(K.k1, XB, wadd(A, C)));
     const uint32_t x3 = wsubk(K.k512_2, F, wmuls<2>(D));
-    const uint32_t y3 = wsubk(K.k1, wf_mul(kn, E, wsubk(K.k1024, D, x3)), wmuls<8>(C));
+    const uint32_t z3 = wsubk(K.k1, YZ2, wadd(B, ZZ));
+    xs[(9 + w) * 64 + l] =
+        w == 0 ? wf_mul(kn, z3, ZZ) : (w == 1 ? wf_mul(kn, E, wsubk(K.k1024, D, x3)) : wmul(EZZ, nxP));
+    tb.sync();
+    const uint32_t y3 = wsubk(K.k1, xs[640 + l], wmuls<8>(C));
+    if (w == 0) {
+      o[0] = wsubk(K.k1, EX, wmuls<2>(B));
+      o[64] = xs[704 + l];
+      o[128] = wmul(xs[576 + l], yP);
+    }
     X = x3;
     Y = y3;
     Z = z3;
-    o[0] = l0;
-    o[64] = l2;
-    o[128] = l3;
   }
-  // addition of Q (affine): T = T + Q, the record into o
-  __device__ void add(const WKG& K, uint32_t* o) {
+  // addition of Q (affine): T = T + Q, the record into o (by the writing wave only, when write)
+  __device__ void add(const WKG& K, uint32_t* o, bool write = true) {
     const uint32_t kn = K.kneg, ks = K.k2048_2;
     const uint32_t z1z1 = wf_sqr(ks, Z);
     const uint32_t u2 = wf_mul(kn, xQ, z1z1);
@@ -566,10 +589,11 @@ struct LineW {
     const uint32_t x3 = wsubk(K.k1, wf_sqr(ks, r), wadd(j, wmuls<2>(v)));
     const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, Y, j)));
     const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Z, h)), wadd(z1z1, hh));
-    const uint32_t l0 = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
-    o[0] = l0;
-    o[64] = wmul(r, nxP);
-    o[128] = wmul(z3, yP);
+    if (write) {
+      o[0] = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
+      o[64] = wmul(r, nxP);
+      o[128] = wmul(z3, yP);
+    }
     X = x3;
     Y = y3;
     Z = z3;
@@ -592,49 +616,49 @@ __constant__ uint8_t FSQ_TERMS[6][4][4] = {  // (i, j, multiplier, xi) ; multipl
     {{0, 5, 2, 0}, {1, 4, 2, 0}, {2, 3, 2, 0}, {0, 0, 0, 0}}};
 
 // Fused per-call Miller loop: waves 0..5 accumulate f (each f^2 and f l as ONE reduction of
-// lazily summed products, f ping-ponging between two LDS banks), wave 6 + p runs pair p's G2 side (LineW) and
-// writes its line records into LDS.  The two sides meet through per-pair progress counters (release / acquire at
+// lazily summed products, f ping-ponging between two LDS banks), waves 6 + 3 p .. 8 + 3 p run pair p's G2 side
+// (LineW, each doubling's products over the three: dbl3) and the first of them writes its line records into LDS.  The two sides meet through per-pair progress counters (release / acquire at
 // workgroup scope); the six f waves synchronise among themselves through a counter barrier, since the line waves
 // never join an s_barrier after the start.  The line records of all steps fit in LDS (2 x 68 x 768 B).
 constexpr int MLF_PAIRS = 2;
-struct WaveBar {  // barrier of the first nw waves of the workgroup: cnt counts arrivals, gen is this wave's target
-  int* cnt;
-  int gen, nw;
-  __device__ void sync() {
-    gen += nw;
-    if (wlane() == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
-  }
-};
 
-__global__ void __launch_bounds__(64 * (6 + MLF_PAIRS)) k_miller_wide(const G1A* P, const G2A* Q, const int* ok0,
-                                                                      const int* ok1, int npairs, Fp12* out) {
+constexpr int MLF_LW = 3;  // line waves per pair
+__global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(const G1A* P, const G2A* Q,
+                                                                               const int* ok0, const int* ok1,
+                                                                               int npairs, Fp12* out) {
   __shared__ uint32_t lr[MLF_PAIRS][MLW_STEPS][3 * 64];
   __shared__ uint32_t fs[2][6 * 64];
+  __shared__ uint32_t xs[MLF_PAIRS][12 * 64];
   __shared__ int prog[MLF_PAIRS];
+  __shared__ int tbc[MLF_PAIRS];
   __shared__ int barc;
   const WKG K = wkg_init();
   const int lane = wlane(), k = (int)(threadIdx.x >> 6);
-  if (threadIdx.x < MLF_PAIRS) prog[threadIdx.x] = 0;
+  if (threadIdx.x < MLF_PAIRS) {
+    prog[threadIdx.x] = 0;
+    tbc[threadIdx.x] = 0;
+  }
   if (threadIdx.x == 0) barc = 0;
   if (k < 6) fs[0][k * 64 + lane] = k == 0 ? wf_from_fp2(fp2_one()) : 0u;
   __syncthreads();
-  if (k >= 6) {  // G2 side of pair k - 6
-    const int pi = k - 6;
-    if (pi >= npairs) return;
+  if (k >= 6) {  // G2 side of pair (k - 6) / 3, wave (k - 6) % 3 of its trio
+    const int pi = (k - 6) / MLF_LW, w3 = (k - 6) % MLF_LW;
+    if (pi >= npairs) return;  // (the whole trio)
     LineW T;
     const int* okp = pi ? ok1 : ok0;
     T.init(P[pi], Q[pi], (!okp || *okp) && !P[pi].inf && !Q[pi].inf);
+    WaveBar tb{&tbc[pi], 0, MLF_LW};
     int step = 0;
 #pragma unroll 1
     for (int b = 62; b >= 0; --b) {
-      T.dbl(K, &lr[pi][step][lane]);
+      T.dbl3(K, &lr[pi][step][lane], xs[pi], w3, tb);
       ++step;
-      if (lane == 0) __hip_atomic_store(&prog[pi], step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (w3 == 0 && lane == 0) __hip_atomic_store(&prog[pi], step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if ((X_ABS >> b) & 1ull) {
-        T.add(K, &lr[pi][step][lane]);
+        T.add(K, &lr[pi][step][lane], w3 == 0);
         ++step;
-        if (lane == 0) __hip_atomic_store(&prog[pi], step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (w3 == 0 && lane == 0)
+          __hip_atomic_store(&prog[pi], step, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     return;
@@ -694,7 +718,7 @@ __global__ void __launch_bounds__(64 * (6 + MLF_PAIRS)) k_miller_wide(const G1A*
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
                               Fp12* out) {
   if (npairs < 1 || npairs > MLF_PAIRS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out);
+  hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out);
   return hipGetLastError();
 }
 
