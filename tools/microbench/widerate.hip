@@ -214,6 +214,38 @@ __global__ void __launch_bounds__(64) k_inv_v(uint32_t* out, int iters) {
   for (int it = 0; it < iters; ++it) x = w_from_fp(fp_inv_sg_i(fp_vgpr(w_to_fp(x))));
   out[threadIdx.x] = x;
 }
+// the cost of one exchange between the waves of a workgroup (LDS write, barrier, LDS read), as the three-wave
+// doublings use it: a dependent chain through the other waves' values, with the s_barrier and with a counter
+// barrier (atomics on LDS + s_sleep polling, as k_miller_wide's f waves and line trios)
+__global__ void __launch_bounds__(192) k_xchg_s(uint32_t* out, int iters) {
+  __shared__ uint32_t xs[3][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  uint32_t v = threadIdx.x;
+  for (int it = 0; it < iters; ++it) {
+    xs[w][l] = v;
+    __syncthreads();
+    v = xs[w == 2 ? 0 : w + 1][l] + 1u;
+    __syncthreads();
+  }
+  out[threadIdx.x] = v;
+}
+__global__ void __launch_bounds__(192) k_xchg_c(uint32_t* out, int iters) {
+  __shared__ uint32_t xs[2][3][64];
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  int gen = 0;
+  uint32_t v = threadIdx.x;
+  for (int it = 0; it < iters; ++it) {
+    xs[it & 1][w][l] = v;  // two buffers: a wave may write round it + 1 while another still reads round it
+    gen += 3;
+    if (l == 0) __hip_atomic_fetch_add(&cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+    v = xs[it & 1][w == 2 ? 0 : w + 1][l] + 1u;
+  }
+  out[threadIdx.x] = v;
+}
 // correctness of the new forms against the old on the same chain (0 = equal)
 __global__ void __launch_bounds__(64) k_check(uint32_t* out, int iters) {
   const WKG K = wkg_init();
@@ -322,6 +354,20 @@ __global__ void __launch_bounds__(192) k_h2c_stages(const uint8_t* msg, uint64_t
 }
 
 template <class K>
+static float run192(K k, uint32_t* d, int iters) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipLaunchKernelGGL(k, dim3(1), dim3(192), 0, 0, d, 16);
+  hipEventRecord(a, 0);
+  hipLaunchKernelGGL(k, dim3(1), dim3(192), 0, 0, d, iters);
+  hipEventRecord(b, 0);
+  hipEventSynchronize(b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+template <class K>
 static float run(K k, uint32_t* d, int iters) {
   hipEvent_t a, b;
   hipEventCreate(&a);
@@ -357,6 +403,8 @@ int main() {
            {"wdot2", run(k_wdot2, d, N), N},
            {"fp_inv_sg_i, SGPR operand", run(k_inv_s, d, 200), 200},
            {"fp_inv_sg_i, VGPR operand", run(k_inv_v, d, 200), 200},
+           {"exchange, s_barrier (x2 per round)", run192(k_xchg_s, d, N), N},
+           {"exchange, counter barrier", run192(k_xchg_c, d, N), N},
            {"wmac walk only", run(k_wmac, d, N), N},
            {"wredc only", run(k_wredc, d, N), N},
            {"fq_mul (lane form, one wave)", run(k_fq, d, N), N}};
