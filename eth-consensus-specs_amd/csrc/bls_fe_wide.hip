@@ -180,7 +180,12 @@ __global__ void __launch_bounds__(384) k_fe_wide(const Fp12* fin, int n, const u
   stamp();
   __shared__ uint32_t B[7 * 6 * 64];
   __shared__ int bad;
-  const int lane = wlane(), k = (int)(threadIdx.x >> 6);
+  // wave w owns coefficient k = w with 3 and 4 swapped.  Six waves on a CU's four SIMDs: waves 0 / 4 and 1 / 5
+  // share a SIMD, 2 and 3 run alone.  A cyclotomic squaring step -- the x-power chains' unit, one barrier each --
+  // costs k = 0: 2 products, 1: 1 + a real one, 2 and 4: 2 + a real one, 3: 1, 5: 1 + a real one; so the shared
+  // SIMDs get {0, 3} and {1, 5} and the two heaviest run alone (a step's slowest SIMD: 3 products instead of
+  // 2 + 2 + a real one with k = w)
+  const int lane = wlane(), wv = (int)(threadIdx.x >> 6), k = wv == 3 ? 4 : (wv == 4 ? 3 : wv);
   if (sel) {
     fin += sel[blockIdx.x];
     out += blockIdx.x;
