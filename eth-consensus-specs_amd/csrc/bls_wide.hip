@@ -62,21 +62,21 @@ __global__ void __launch_bounds__(64) k_wide_selftest(size_t nw, const uint8_t* 
   if (threadIdx.x == 0) bad[w] = mh | (mo << 10);
 }
 
-// hash_to_G2 of item blockIdx.x on one workgroup of three waves (per-call path), every wave doing the same work
-// except the cofactor chains' doublings, whose products are spread over the three (j2f_dbl3, bls_wide_g2.h:
-// a doubling in three product rounds instead of seven): hash_to_field on every lane (uniform), the SSWU map
+// hash_to_G2 of item blockIdx.x on one workgroup of four waves (per-call path), every wave doing the same work
+// except the cofactor chains' doublings, whose products are spread over the four (p2f_dbl4, bls_wide_g2.h: the
+// complete projective doubling in two product rounds): hash_to_field on every lane (uniform), the SSWU map
 // and 3-isogeny of u_0 in half 0 and of u_1 in half 1, their sum, the cofactor clearing
 //   H = [x^2 - x - 1] Q + [x - 1] psi(Q) + psi^2(2 Q)  as  M = [|x|] Q,  A' = M - psi(Q),
 //   C = psi^2(2 Q) - psi(Q) + M - Q,  H = C + [|x|] A'   (A' = -A of k_g2x_pre1t / k_g2x_post1t)
-// in both halves (two Jacobian representations of the same points), and the affine H from half 0.  flag[i] = 1
-// for the cases the fallback recomputes (SSWU `rare`, a vanishing isogeny denominator, an exceptional addition).
+// in complete projective formulas (F2 layout), and the affine H.  flag[i] = 1 for the cases the fallback
+// recomputes (SSWU `rare`, a vanishing isogeny denominator, an exceptional P0 + P1).
 // msgs: 32-byte messages msgs[32 i ..] (offs == nullptr) or msgs[offs[i] .. offs[i+1]).
-__global__ void __launch_bounds__(192) k_h2c_wide(size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H,
+__global__ void __launch_bounds__(256) k_h2c_wide(size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H,
                                                   int* flag) {
   const size_t i = blockIdx.x;
   if (i >= B) return;  // (the whole workgroup)
-  __shared__ uint32_t x3[6 * 64];
-  const int w = (int)(threadIdx.x >> 6);  // three waves: the same work up to the cofactor chains' doublings
+  __shared__ uint32_t x4[8 * 64];
+  const int w = (int)(threadIdx.x >> 6);  // four waves: the same work up to the cofactor chains' doublings
   const WKG K = wkg_init();
   Fp2 u[2];
   if (offs)
@@ -94,16 +94,17 @@ __global__ void __launch_bounds__(192) k_h2c_wide(size_t B, const uint8_t* msgs,
   const J2F Q = j2f_of_j2w(j2w_add(K, P, Po, exc));
   const uint32_t cx = wf_from_fp2(PSI_CX), cy = wf_from_fp2(PSI_CY);
   const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
-  const J2F M = j2f_mul_xabs3(K, Q, exc, x3, w);
-  const J2F npq = j2f_neg(K, j2f_psi(K, Q, cx, cy));
-  const J2F Ap = j2f_add(K, M, npq, exc);
-  J2F C = j2f_add(K, j2f_psi2(j2f_dbl(K, Q), c2x, c2y), npq, exc);
-  C = j2f_add(K, C, M, exc);
-  C = j2f_add(K, C, j2f_neg(K, Q), exc);
-  const J2F M2 = j2f_mul_xabs3(K, Ap, exc, x3, w);
-  if (w) return;  // waves 1, 2: no barrier after the chains
-  const J2F Hj = j2f_add(K, C, M2, exc);
-  const G2A h = j2f_to_aff(K, Hj);
+  // the cofactor clearing in complete projective formulas (P2F): no exceptional case after P0 + P1
+  const P2F Qp = p2f_of_j2f(K, Q);
+  const P2F M = p2f_mul_xabs4(K, Qp, x4, w);
+  const P2F npq = p2f_neg(K, p2f_psi(K, Qp, cx, cy));
+  const P2F Ap = p2f_add(K, M, npq);
+  P2F C = p2f_add(K, p2f_psi2(p2f_dbl4(K, Qp, x4, w), c2x, c2y), npq);
+  C = p2f_add(K, C, M);
+  C = p2f_add(K, C, p2f_neg(K, Qp));
+  const P2F M2 = p2f_mul_xabs4(K, Ap, x4, w);
+  if (w) return;  // waves 1 .. 3: no barrier after the chains
+  const G2A h = p2f_to_aff(K, p2f_add(K, C, M2));
   const int bad = (rare | izero | exc) ? 1 : 0;
   const int bad_any = __builtin_amdgcn_readlane(bad, 0) | __builtin_amdgcn_readlane(bad, 32);
   if (threadIdx.x == 0) {
@@ -282,7 +283,7 @@ hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out) {
 
 hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_h2c_wide, dim3((unsigned)B), dim3(192), 0, st, B, msgs, offs, H, flag);
+  hipLaunchKernelGGL(k_h2c_wide, dim3((unsigned)B), dim3(256), 0, st, B, msgs, offs, H, flag);
   return hipGetLastError();
 }
 

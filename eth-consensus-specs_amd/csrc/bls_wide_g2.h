@@ -282,76 +282,120 @@ __device__ __forceinline__ J2F j2f_mul_xabs(const WKG& K, const J2F& p, bool& ex
   }
   return m;
 }
-// The same doubling on THREE waves of one workgroup (the per-call hash's cofactor chains, k_h2c_wide): its seven
-// F2 products have dependency depth 3 -- {A = X^2, B = Y^2, YZ = Y Z}, {C = B^2, XB2 = (X + B)^2, EE = (3A)^2},
-// {E (D - X3)} -- so wave w forms product w of each of the first two levels, the waves exchange them through LDS
-// (one barrier per level), and every wave forms the last product itself.  Each wave ends with the whole point,
-// the same values as j2f_dbl's.  x3: 6 x 64 words of LDS; w: this wave's index (0, 1, 2), uniform per wave.
-__device__ __forceinline__ J2F j2f_dbl3(const WKG& K, const J2F& p, uint32_t* x3, int w) {
-  const uint32_t ks = K.k2048_2, kn = K.kneg;
+// ---- G2 homogeneous projective in F2 layout: the complete formulas of bls_pp_lane.h (Renes-Costello-Batina,
+// a = 0, 3b = 12 (1 + i)) as the round-4 wide MSM kernel ran them -- no exceptional cases, so the per-call
+// hash's cofactor chains need no fallback flag, and a doubling's eight products have dependency depth 2.
+struct P2F {  // (X : Y : Z), every coordinate a product output (< 2.0001 p) on entry to the formulas
+  uint32_t x, y, z;
+};
+// 3 b t = 12 xi t (t below 62 p: the xi subtraction against 64 p)
+__device__ __forceinline__ uint32_t wf_b3(const WKG& K, uint32_t t) { return wmuls<12>(wf_xi(K.k1, t)); }
+
+// pp_dbl on FOUR waves of one workgroup (w = 0 .. 3, uniform per wave): t0 = Y^2, t1 = Y Z, Z^2, u = X Y (one per
+// wave), then t2 = 3b Z^2, z8 = 8 t0, w = t0 - 3 t2 and X3 = 2 w u, Y3 = w (t0 + t2) + t2 z8 (one reduction of two
+// products), Z3 = t1 z8 (waves 1, 0, 2), exchanged through x4 (8 x 64 words) with one barrier per level.
+// Bounds (units of p): t0, t1, Z^2, u < 2.0001; t2 < 1500; w < 4100 (against 4096 p covering 3 t2 < 4096 p)
+__device__ __forceinline__ P2F p2f_dbl4(const WKG& K, const P2F& p, uint32_t* x4, int w) {
+  const uint32_t kn = K.kneg;
   const int l = wlane();
   uint32_t m1;
   if (w == 0)
-    m1 = wf_sqr(ks, p.x);
+    m1 = wf_sqr(K.k1, p.y);
   else if (w == 1)
-    m1 = wf_sqr(ks, p.y);
-  else
     m1 = wf_mul(kn, p.y, p.z);
-  x3[w * 64 + l] = m1;
-  __syncthreads();
-  const uint32_t A = x3[l], Bq = x3[64 + l], YZ = x3[128 + l];
-  const uint32_t E = wmuls<3>(A);
-  uint32_t m2;
-  if (w == 0)
-    m2 = wf_sqr(ks, Bq);
-  else if (w == 1)
-    m2 = wf_sqr(ks, wadd(p.x, Bq));
+  else if (w == 2)
+    m1 = wf_sqr(K.k1, p.z);
   else
-    m2 = wf_sqr(ks, E);
-  x3[(3 + w) * 64 + l] = m2;
+    m1 = wf_mul(kn, p.x, p.y);
+  x4[w * 64 + l] = m1;
   __syncthreads();
-  const uint32_t C = x3[192 + l], XB2 = x3[256 + l], EE = x3[320 + l];
-  const uint32_t D = wmuls<2>(wsubk(K.k2, XB2, wadd(A, C)));
-  J2F r;
-  r.x = wsubk(K.k1024, EE, wmuls<2>(D));
-  const uint32_t DX = wsubk(K.k2048_2, D, r.x);
-  r.y = wsubk(K.k1, wf_mul(kn, E, DX), wmuls<8>(C));
-  r.z = wmuls<2>(YZ);
+  const uint32_t t0 = x4[l], t1 = x4[64 + l], t2 = wf_b3(K, x4[128 + l]), u = x4[192 + l];
+  const uint32_t z8 = wmuls<8>(t0);
+  const uint32_t wv = wsubk(kn, t0, wmuls<3>(t2));
+  if (w == 0) {
+    uint64_t acc = 0;
+    wf_mac(acc, kn, wv, wadd(t0, t2));
+    wf_mac(acc, kn, t2, z8);
+    x4[256 + l] = wredc(acc);
+  } else if (w == 1) {
+    x4[320 + l] = wf_mul(kn, wv, wmuls<2>(u));
+  } else if (w == 2) {
+    x4[384 + l] = wf_mul(kn, t1, z8);
+  }
+  __syncthreads();
+  return P2F{x4[320 + l], x4[256 + l], x4[384 + l]};
+}
+
+// pp_add / pp_finish with the cross terms as sums of products (t3 = X1 Y2 + Y1 X2, ...):
+//   X3 = t3 t1' - t4 y3',  Y3 = t1' z3 + y3' 3 t0,  Z3 = z3 t4 + 3 t0 t3   (t1' = t1 - 3b t2, z3 = t1 + 3b t2,
+//   y3' = 3b y3), each output one reduction; the big operands (y3' < 790 p) go first, the negated t4 (< 256 p)
+//   second, inside kneg's 4096 p.  Every wave computes it (the chains' additions are few).
+__device__ __forceinline__ P2F p2f_add(const WKG& K, const P2F& p, const P2F& q) {
+  const uint32_t kn = K.kneg;
+  const uint32_t t0 = wf_mul(kn, p.x, q.x);
+  const uint32_t t1 = wf_mul(kn, p.y, q.y);
+  const uint32_t t2 = wf_mul(kn, p.z, q.z);
+  uint64_t a3 = 0, a4 = 0, ay = 0;
+  wf_mac(a3, kn, p.x, q.y);
+  wf_mac(a3, kn, p.y, q.x);
+  wf_mac(a4, kn, p.y, q.z);
+  wf_mac(a4, kn, p.z, q.y);
+  wf_mac(ay, kn, p.x, q.z);
+  wf_mac(ay, kn, p.z, q.x);
+  const uint32_t t3 = wredc(a3), t4 = wredc(a4), y3 = wf_b3(K, wredc(ay));
+  const uint32_t bt2 = wf_b3(K, t2);
+  const uint32_t t0x3 = wmuls<3>(t0);
+  const uint32_t z3 = wadd(t1, bt2);
+  const uint32_t t1m = wsubk(K.k1024, t1, bt2);
+  P2F r;
+  uint64_t ax = 0, ayy = 0, az = 0;
+  wf_mac(ax, kn, t3, t1m);
+  wf_mac(ax, kn, y3, wsubk(K.k256, 0u, t4));
+  wf_mac(ayy, kn, t1m, z3);
+  wf_mac(ayy, kn, y3, t0x3);
+  wf_mac(az, kn, z3, t4);
+  wf_mac(az, kn, t0x3, t3);
+  r.x = wredc(ax);
+  r.y = wredc(ayy);
+  r.z = wredc(az);
   return r;
 }
-// [|x|] p with the doublings on three waves (the additions on every wave)
-__device__ __forceinline__ J2F j2f_mul_xabs3(const WKG& K, const J2F& p, bool& exc, uint32_t* x3, int w) {
-  J2F m = p;
+// [|x|] p with the doublings on four waves (the additions on every wave)
+__device__ __forceinline__ P2F p2f_mul_xabs4(const WKG& K, const P2F& p, uint32_t* x4, int w) {
+  P2F m = p;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
-    m = j2f_dbl3(K, m, x3, w);
-    if ((X_ABS >> b) & 1ull) m = j2f_add(K, m, p, exc);
+    m = p2f_dbl4(K, m, x4, w);
+    if ((X_ABS >> b) & 1ull) m = p2f_add(K, m, p);
   }
   return m;
 }
-__device__ __forceinline__ J2F j2f_neg(const WKG& K, const J2F& p) {
-  return J2F{p.x, wsubk(K.k1, 0u, wmul(p.y, K.one)), p.z};
+// Jacobian (X, Y, Z) (F2 layout, the chain bounds of J2F) -> projective (X Z, Y, Z^3), every coordinate a product
+__device__ __forceinline__ P2F p2f_of_j2f(const WKG& K, const J2F& p) {
+  const uint32_t zz = wf_sqr(K.k2048_2, p.z);
+  return P2F{wf_mul(K.kneg, p.x, p.z), wmul(p.y, K.one), wf_mul(K.kneg, zz, p.z)};
 }
-// psi(P) = (conj(X) cx, conj(Y) cy, conj(Z)); cx, cy in F2 layout
-__device__ __forceinline__ J2F j2f_psi(const WKG& K, const J2F& p, uint32_t cx, uint32_t cy) {
+// -P (the negated Y brought back to a product output)
+__device__ __forceinline__ P2F p2f_neg(const WKG& K, const P2F& p) {
+  return P2F{p.x, wmul(wsubk(K.k1, 0u, p.y), K.one), p.z};
+}
+// psi(P) = (conj(X) cx : conj(Y) cy : conj(Z)) (cx, cy in F2 layout; as on Jacobian coordinates)
+__device__ __forceinline__ P2F p2f_psi(const WKG& K, const P2F& p, uint32_t cx, uint32_t cy) {
   const uint32_t zc = wmul(wf_conj(K.k2048_2, p.z), K.one);
-  return J2F{wf_mul(K.kneg, wf_conj(K.k2048_2, p.x), cx), wf_mul(K.kneg, wf_conj(K.k2048_2, p.y), cy), zc};
+  return P2F{wf_mul(K.kneg, wf_conj(K.k2048_2, p.x), cx), wf_mul(K.kneg, wf_conj(K.k2048_2, p.y), cy), zc};
 }
-// psi^2(P) = (X c2x, Y c2y, Z) (c2x, c2y in Fp, both halves)
-__device__ __forceinline__ J2F j2f_psi2(const J2F& p, uint32_t c2x, uint32_t c2y) {
-  return J2F{wmul(p.x, c2x), wmul(p.y, c2y), p.z};
+// psi^2(P) = (X c2x : Y c2y : Z) (c2x, c2y in Fp, both halves)
+__device__ __forceinline__ P2F p2f_psi2(const P2F& p, uint32_t c2x, uint32_t c2y) {
+  return P2F{wmul(p.x, c2x), wmul(p.y, c2y), p.z};
 }
-// Jacobian -> affine (x, y) canonical packed; the identity (Z = 0) -> inf
-__device__ __forceinline__ G2A j2f_to_aff(const WKG& K, const J2F& p) {
-  const uint32_t sq = wsqr(p.z);  // z0^2 | z1^2
-  const uint32_t nz = wadd(sq, wswap(sq));  // norm(Z) in both halves
-  const Fp nl = w_to_fp(nz);
+// (X : Y : Z) -> (X / Z, Y / Z) canonical packed; Z = 0 (the identity) -> inf
+__device__ __forceinline__ G2A p2f_to_aff(const WKG& K, const P2F& p) {
+  const uint32_t sq = wsqr(p.z);
+  const Fp nl = w_to_fp(wadd(sq, wswap(sq)));  // norm(Z) in both halves
   G2A r{fp2_zero(), fp2_zero(), true};
   const uint32_t ni = w_from_fp(fp_inv_sg_i(nl));
   const uint32_t zi = wmul(wf_conj(K.k2048_2, p.z), ni);
-  const uint32_t zi2 = wf_mul(K.kneg, zi, zi);
-  const uint32_t zi3 = wf_mul(K.kneg, zi2, zi);
-  const Fp2 x = wf_to_fp2(wf_mul(K.kneg, p.x, zi2)), y = wf_to_fp2(wf_mul(K.kneg, p.y, zi3));
+  const Fp2 x = wf_to_fp2(wf_mul(K.kneg, p.x, zi)), y = wf_to_fp2(wf_mul(K.kneg, p.y, zi));
   if (!fp_is_zero(nl)) r = G2A{x, y, false};
   return r;
 }

@@ -312,9 +312,9 @@ __global__ void __launch_bounds__(64) k_fq(uint32_t* out, int iters) {
   out[threadIdx.x] = x.d[0] ^ x.d[13];
 }
 
-// k_h2c_wide (bls_wide.hip, three waves) on one 32-byte message with wall-clock stamps (100 MHz) between its stages
-__global__ void __launch_bounds__(192) k_h2c_stages(const uint8_t* msg, uint64_t* ts, uint32_t* out) {
-  __shared__ uint32_t x3[6 * 64];
+// k_h2c_wide (bls_wide.hip, four waves) on one 32-byte message with wall-clock stamps (100 MHz) between its stages
+__global__ void __launch_bounds__(256) k_h2c_stages(const uint8_t* msg, uint64_t* ts, uint32_t* out) {
+  __shared__ uint32_t x4[8 * 64];
   const int w = (int)(threadIdx.x >> 6);
   uint64_t t[10];
   t[0] = wall_clock64();
@@ -334,18 +334,18 @@ __global__ void __launch_bounds__(192) k_h2c_stages(const uint8_t* msg, uint64_t
   t[3] = wall_clock64();
   const uint32_t cx = wf_from_fp2(PSI_CX), cy = wf_from_fp2(PSI_CY);
   const uint32_t c2x = w_from_fp(PSI2_CX.c0), c2y = w_from_fp(PSI2_CY.c0);
-  const J2F M = j2f_mul_xabs3(K, Q, exc, x3, w);
+  const P2F Qp = p2f_of_j2f(K, Q);
+  const P2F M = p2f_mul_xabs4(K, Qp, x4, w);
   t[4] = wall_clock64();
-  const J2F npq = j2f_neg(K, j2f_psi(K, Q, cx, cy));
-  const J2F Ap = j2f_add(K, M, npq, exc);
-  J2F C = j2f_add(K, j2f_psi2(j2f_dbl(K, Q), c2x, c2y), npq, exc);
-  C = j2f_add(K, C, M, exc);
-  C = j2f_add(K, C, j2f_neg(K, Q), exc);
+  const P2F npq = p2f_neg(K, p2f_psi(K, Qp, cx, cy));
+  const P2F Ap = p2f_add(K, M, npq);
+  P2F C = p2f_add(K, p2f_psi2(p2f_dbl4(K, Qp, x4, w), c2x, c2y), npq);
+  C = p2f_add(K, C, M);
+  C = p2f_add(K, C, p2f_neg(K, Qp));
   t[5] = wall_clock64();
-  const J2F M2 = j2f_mul_xabs3(K, Ap, exc, x3, w);
+  const P2F M2 = p2f_mul_xabs4(K, Ap, x4, w);
   t[6] = wall_clock64();
-  const J2F Hj = j2f_add(K, C, M2, exc);
-  const G2A h = j2f_to_aff(K, Hj);
+  const G2A h = p2f_to_aff(K, p2f_add(K, C, M2));
   t[7] = wall_clock64();
   if (threadIdx.x == 0) {
     for (int k = 0; k < 8; ++k) ts[k] = t[k];
@@ -445,7 +445,7 @@ int main() {
   const char* st[7] = {"hash_to_field", "sswu (u0 | u1)", "iso + P0 + P1", "M = [|x|] Q", "psi terms, C", "M2 = [|x|] A'",
                        "H, affine"};
   for (int rep = 0; rep < 3; ++rep) {
-    hipLaunchKernelGGL(k_h2c_stages, dim3(1), dim3(192), 0, 0, dm, dts, d);
+    hipLaunchKernelGGL(k_h2c_stages, dim3(1), dim3(256), 0, 0, dm, dts, d);
     CK(hipDeviceSynchronize());
   }
   uint64_t hts[8];
