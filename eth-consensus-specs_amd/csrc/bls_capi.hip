@@ -193,6 +193,18 @@ int d2h(bls_ctx* ctx, void* h, const void* d, size_t n) {
   } while (0)
 
 constexpr size_t WIDE_H2C_MAX = 512;  // AggregateVerify: one wave per message up to this many
+// the Miller values of the per-call pairing APIs (AggregateVerify, pairing checks, multi-pairings): the wide kernel
+// on ceil(n / 2) workgroups up to this many pairs (a workgroup per CU at most), the wave-program kernel beyond;
+// *nf = the number of f values written
+constexpr size_t WIDE_MILLER_MAX = 512;
+static hipError_t launch_miller_call(hipStream_t st, const G1A* P, const G2A* Q, size_t n, Fp12* f, size_t* nf) {
+  if (n <= WIDE_MILLER_MAX) {
+    *nf = (n + 1) / 2;
+    return launch_miller_wide_n(st, P, Q, nullptr, n, f);
+  }
+  *nf = n;
+  return launch_miller_wave(st, P, Q, nullptr, n, f);
+}
 constexpr size_t WIDE_KEYS_MAX = 4096;  // KeyValidate of a call's keys: two keys per wave up to this many
 
 // a call's keys (per-call FastAggregateVerify, AggregateVerify, AggregatePKs): the wide kernel's latency for a few
@@ -644,8 +656,9 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st, P + n);
   LK(hipGetLastError());
-  LK(launch_miller_wave(st, P, Q, nullptr, n + 1, f));  // a rejected signature is the identity there
-  LK(launch_fp12_prod_vm(st, f, n + 1, ft, fo));
+  size_t nf = 0;
+  LK(launch_miller_call(st, P, Q, n + 1, f, &nf));  // a rejected signature: constant lines there
+  LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
   PROF2(7, st, launch_fe_wide(st, fo, 1, d_w + 1));
   int w[2] = {0, 0};
   CK(d2h(ctx, w, d_w, sizeof w));
@@ -1605,8 +1618,9 @@ int bls_pairing_check(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, 
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
   for (size_t i = 0; i < n; i++)
     if (!a[i] || !b[i]) return 0;
-  LK(launch_miller_wave(st, P, Q, nullptr, n, f));  // identity pairs are skipped (value 1)
-  LK(launch_fp12_prod_vm(st, f, n, ft, fo));
+  size_t nf = 0;
+  LK(launch_miller_call(st, P, Q, n, f, &nf));  // identity pairs: an Fp2 factor, 1 after the final exponentiation
+  LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
   return run_final_check(ctx, fo);
 }
 
@@ -1773,8 +1787,9 @@ int bls_multi_pairing(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, 
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
   for (size_t i = 0; i < n; i++)
     if (!a[i] || !b[i]) return 0;
-  LK(launch_miller_wave(st, P, Q, nullptr, n, f));  // identity pairs contribute 1
-  LK(launch_fp12_prod_vm(st, f, n, ft, fo));
+  size_t nf = 0;
+  LK(launch_miller_call(st, P, Q, n, f, &nf));  // identity pairs: an Fp2 factor, 1 after the final exponentiation
+  LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
   LK(launch_gt_final_exp(st, fo, d_out));
   CK(d2h(ctx, out576, d_out, 576));
   return 1;
@@ -1821,8 +1836,9 @@ int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s9
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
   for (size_t i = 0; i < n; i++)
     if (!a[i] || !b[i]) return 0;
-  LK(launch_miller_wave(st, P, Q, nullptr, n, f));
-  LK(launch_fp12_prod_vm(st, f, n, ft, fo));
+  size_t nf = 0;
+  LK(launch_miller_call(st, P, Q, n, f, &nf));
+  LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
   return run_final_check(ctx, fo);
 }
 

@@ -624,9 +624,21 @@ __constant__ uint8_t FSQ_TERMS[6][4][4] = {  // (i, j, multiplier, xi) ; multipl
 constexpr int MLF_PAIRS = 2;
 
 constexpr int MLF_LW = 3;  // line waves per pair
+// okv != nullptr (launch_miller_wide_n): workgroup b runs pairs 2b, 2b + 1 of npairs (okv per pair, or none)
+// into out[b]; otherwise one workgroup, npairs <= 2, ok0 / ok1 per pair
 __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(const G1A* P, const G2A* Q,
                                                                                const int* ok0, const int* ok1,
-                                                                               int npairs, Fp12* out) {
+                                                                               int npairs, Fp12* out,
+                                                                               const int* okv, int per_block) {
+  if (per_block) {
+    const int b = (int)blockIdx.x;
+    P += MLF_PAIRS * b;
+    Q += MLF_PAIRS * b;
+    out += b;
+    ok0 = okv ? okv + MLF_PAIRS * b : nullptr;
+    ok1 = okv ? okv + MLF_PAIRS * b + 1 : nullptr;
+    npairs = npairs - MLF_PAIRS * b < MLF_PAIRS ? npairs - MLF_PAIRS * b : MLF_PAIRS;
+  }
   __shared__ uint32_t lr[MLF_PAIRS][MLW_STEPS][3 * 64];
   __shared__ uint32_t fs[2][6 * 64];
   __shared__ uint32_t xs[MLF_PAIRS][12 * 64];
@@ -719,7 +731,18 @@ __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(c
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
                               Fp12* out) {
   if (npairs < 1 || npairs > MLF_PAIRS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out);
+  hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out,
+                     nullptr, 0);
+  return hipGetLastError();
+}
+
+// n pairs on ceil(n / 2) workgroups of k_miller_wide (one f per workgroup, out[0 .. (n + 1) / 2)): the latency of
+// one wide Miller loop for a few hundred pairs, where the lane kernels' chains take ~2 ms whatever n
+hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out) {
+  if (!n) return hipSuccess;
+  if (n > (size_t)1 << 20) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_miller_wide, dim3((unsigned)((n + MLF_PAIRS - 1) / MLF_PAIRS)),
+                     dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, nullptr, nullptr, (int)n, out, ok, 1);
   return hipGetLastError();
 }
 
