@@ -192,11 +192,14 @@ int d2h(bls_ctx* ctx, void* h, const void* d, size_t n) {
     if (e_ != hipSuccess) return fail(ctx, e_, #x);             \
   } while (0)
 
-constexpr size_t WIDE_H2C_MAX = 512;  // AggregateVerify: one wave per message up to this many
+// AggregateVerify: one wide workgroup per message up to this many (tools/av_probe.py: 1,024 messages 7.95 -> 6.85
+// ms; 8,192 took 15.1 -> 31.5 ms, past the chip's CUs); knob BLS_WIDE_H2C_MAX
+static const size_t WIDE_H2C_MAX = getenv("BLS_WIDE_H2C_MAX") ? (size_t)atol(getenv("BLS_WIDE_H2C_MAX")) : 1024;
 // the Miller values of the per-call pairing APIs (AggregateVerify, pairing checks, multi-pairings): the wide kernel
-// on ceil(n / 2) workgroups up to this many pairs (a workgroup per CU at most), the wave-program kernel beyond;
-// *nf = the number of f values written
-constexpr size_t WIDE_MILLER_MAX = 512;
+// on ceil(n / 2) workgroups up to this many pairs, the wave-program kernel beyond (AggregateVerify(512) 5.54 -> 4.17
+// ms, (1,024) 7.95 -> 7.31; at 8,192 pairs the wave programs' throughput wins); *nf = the number of f values written;
+// knob BLS_WIDE_MILLER_MAX
+static const size_t WIDE_MILLER_MAX = getenv("BLS_WIDE_MILLER_MAX") ? (size_t)atol(getenv("BLS_WIDE_MILLER_MAX")) : 1100;
 static hipError_t launch_miller_call(hipStream_t st, const G1A* P, const G2A* Q, size_t n, Fp12* f, size_t* nf) {
   if (n <= WIDE_MILLER_MAX) {
     *nf = (n + 1) / 2;
@@ -636,7 +639,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   HIPCK(hipEventRecord(J.ev_sig, ss));
   bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
   for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
-  if (n <= WIDE_H2C_MAX)  // a few messages: one wave each, lower latency than the lane kernels' chains
+  if (n <= WIDE_H2C_MAX)  // up to ~a thousand messages: one wide workgroup each, lower latency than the lane chains
     LK(launch_h2c_wide(st2, n, d_msgs, m32 ? nullptr : d_offs, Q, d_flag));
   else if (m32)
     LK(launch_h2c(st2, n, d_msgs, nullptr, d_hf, Q, d_flag));
