@@ -216,6 +216,19 @@ static hipError_t launch_keys(hipStream_t st, const uint8_t* pks, size_t n, G1A*
   return n <= WIDE_KEYS_MAX ? launch_key_validate_wide(st, pks, n, out, ok) : launch_key_validate(st, pks, n, out, ok);
 }
 
+// the pairing APIs' decodes of n (G1, G2) pairs at d_in (48 n bytes of G1, then 96 n of G2), identity accepted: with
+// the subgroup checks on the wide kernels (latency; up to WIDE_KEYS_MAX pairs), unchecked or beyond on the lane kernels
+static hipError_t launch_pairs_decode(hipStream_t st, const uint8_t* d_in, size_t n, bool subgroup, G1A* P, G2A* Q,
+                                      int* ok1, int* ok2) {
+  hipError_t e;
+  if (subgroup && n <= WIDE_KEYS_MAX) {
+    e = launch_g1_decode_checked_wide(st, d_in, n, P, ok1);
+    return e != hipSuccess ? e : launch_sig_validate_wide(st, d_in + 48 * n, n, Q, ok2);
+  }
+  e = launch_pt_decode(st, 1, d_in, n, subgroup ? 1 : 0, P, ok1);
+  return e != hipSuccess ? e : launch_pt_decode(st, 2, d_in + 48 * n, n, subgroup ? 1 : 0, Q, ok2);
+}
+
 // Copy n compressed keys, validate them on the device; returns 1 if all valid.
 int validate_pks(bls_ctx* ctx, const uint8_t* pks, size_t n, G1A** outA, int** outOk) {
   uint8_t* d_in;
@@ -285,7 +298,7 @@ void prof_collect(bls_ctx* c) {
 
 // Final-exponentiation check of the product of f[0 .. n) on the context's FE
 // stream, after the current job's stream: 1 / 0.
-int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
+int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1, bool wide = false) {
   int* d_r;
   SCR(S_INT, 4, d_r);
   Job& J = *ctx->j;
@@ -296,8 +309,11 @@ int run_final_check(bls_ctx* ctx, const Fp12* f, int n = 1) {
     HIPCK(hipStreamWaitEvent(fe, J.ev_fe, 0));
   }
   // batch checks on the one-wave k_fe_check, which leaves the CU to the other jobs (profiles/r04m_fe_ab.txt: 1.92 M vs
-  // 1.84 M FAV/s with every check six-wave); the per-call path runs k_fe_wide on its own stream (verify_percall)
-  PROF2(7, fe, launch_final_check_wave(fe, f, n, d_r));
+  // 1.84 M FAV/s with every check six-wave); single calls (wide: the pairing checks) on the six-wave k_fe_wide
+  if (wide)
+    PROF2(7, fe, launch_fe_wide(fe, f, n, d_r));
+  else
+    PROF2(7, fe, launch_final_check_wave(fe, f, n, d_r));
   int r = 0;
   HIPCK(hipMemcpyAsync(&r, d_r, sizeof r, hipMemcpyDeviceToHost, fe));
   HIPCK(hipStreamSynchronize(fe));
@@ -1403,6 +1419,9 @@ static int fav_batch_host(bls_ctx* ctx, const uint32_t* idx, const uint64_t* off
   CK(h2d(ctx, d_s, sigs96, 96 * B));
   uint8_t seed[32];
   CK(host_seed(ctx, seed));
+  // the inputs were just copied on stream1: the hash on stream2 forks after them, never from a bisection's ev_bis
+  // (an earlier call's, recorded before these copies; the hash would read the previous contents of S_IN1)
+  ctx->j->bis_pending = false;
   Fp12* f;
   CK(fav_prepare(ctx, d_idx, d_offs, B, d_m, d_s, seed, &f));
   int ok = run_final_check(ctx, f);
@@ -1614,8 +1633,7 @@ int bls_pairing_check(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, 
   SCR(S_FPART, 1, fo);
   CK(h2d(ctx, d_in, g1s48, 48 * n));
   CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
-  LK(launch_g1_decode_checked(st, d_in, n, P, ok1));
-  LK(launch_sig_validate(st, d_in + 48 * n, n, Q, ok2));
+  LK(launch_pairs_decode(st, d_in, n, true, P, Q, ok1, ok2));
   std::vector<int> a(n), b(n);
   CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
@@ -1624,7 +1642,7 @@ int bls_pairing_check(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, 
   size_t nf = 0;
   LK(launch_miller_call(st, P, Q, n, f, &nf));  // identity pairs: an Fp2 factor, 1 after the final exponentiation
   LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
-  return run_final_check(ctx, fo);
+  return run_final_check(ctx, fo, 1, true);
 }
 
 int bls_g1_multi_exp(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* scalars32, size_t n, uint8_t* out48) {
@@ -1783,8 +1801,7 @@ int bls_multi_pairing(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, 
   SCR(S_PT_OUT, 576, d_out);
   CK(h2d(ctx, d_in, g1s48, 48 * n));
   CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
-  LK(launch_pt_decode(st, 1, d_in, n, subgroup_check ? 1 : 0, P, ok1));
-  LK(launch_pt_decode(st, 2, d_in + 48 * n, n, subgroup_check ? 1 : 0, Q, ok2));
+  LK(launch_pairs_decode(st, d_in, n, subgroup_check != 0, P, Q, ok1, ok2));
   std::vector<int> a(n), b(n);
   CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
@@ -1832,8 +1849,7 @@ int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s9
   SCR(S_FPART, 1, fo);
   CK(h2d(ctx, d_in, g1s48, 48 * n));
   CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
-  LK(launch_pt_decode(st, 1, d_in, n, subgroup_check ? 1 : 0, P, ok1));
-  LK(launch_pt_decode(st, 2, d_in + 48 * n, n, subgroup_check ? 1 : 0, Q, ok2));
+  LK(launch_pairs_decode(st, d_in, n, subgroup_check != 0, P, Q, ok1, ok2));
   std::vector<int> a(n), b(n);
   CK(d2h(ctx, a.data(), ok1, n * sizeof(int)));
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
@@ -1842,7 +1858,7 @@ int bls_pairing_check_ex(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s9
   size_t nf = 0;
   LK(launch_miller_call(st, P, Q, n, f, &nf));
   LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
-  return run_final_check(ctx, fo);
+  return run_final_check(ctx, fo, 1, true);
 }
 
 int bls_last_fallback_stats(bls_ctx* ctx, uint64_t* fe_checks, uint64_t* rounds) {

@@ -131,5 +131,7 @@ hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, cons
 hipError_t launch_fe_wide(hipStream_t st, const Fp12* f, int n, int* out, uint64_t* ts = nullptr);  // ts: stage clocks (tests)
 // KeyValidate with two keys per wave (k_key_validate semantics)
 hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok);
+// the checked G1 decode (identity accepted, k_pt_decode semantics) on the wide KeyValidate kernel
+hipError_t launch_g1_decode_checked_wide(hipStream_t st, const uint8_t* in48, size_t n, G1A* out, int* ok);
 
 }  // namespace bls

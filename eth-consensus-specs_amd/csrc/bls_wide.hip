@@ -460,7 +460,9 @@ __device__ __forceinline__ G1W g1w_mul_xabs4(const WKG& K, const G1W& b, uint32_
 // KeyValidate of keys 2 blockIdx.x + half (k_key_validate semantics; the decode on every lane of the half, the
 // square root and both [|x|] chains in wide arithmetic), on a workgroup of four waves doing the same work except
 // the chains' doublings, whose products are spread over the four (g1w_dbl4).  Wave-uniform control flow: the two
-// halves' decode verdicts are combined into selects, not branches.
+// halves' decode verdicts are combined into selects, not branches.  INF_OK: the checked G1 decode of the pairing APIs
+// (k_pt_decode semantics: the identity encoding is a valid point) instead of KeyValidate's rejection of it.
+template <bool INF_OK>
 __global__ void __launch_bounds__(256) k_key_validate_wide(const uint8_t* pks48, size_t n, G1A* out, int* ok) {
   const size_t base = 2 * (size_t)blockIdx.x;
   if (base >= n) return;  // (the whole workgroup)
@@ -494,16 +496,23 @@ __global__ void __launch_bounds__(256) k_key_validate_wide(const uint8_t* pks48,
   const bool eq_x = w_eq(K1, wmul(wmul(xm, w_from_fp(FP_BETA)), Q.z), wmul(Q.x, K.one));
   const bool eq_y = w_is_zero(wadd(wmul(y, Q.z), Q.y));
   const bool v = fmt && on && eq_x && eq_y;
+  const bool id = INF_OK && c_flag && b_flag && !a_flag && fp_is_zero(x);
   const G1A a = v ? G1A{w_to_fp(xm), w_to_fp(y), false} : G1A{fp_zero(), fp_zero(), true};
   if (wpos() == 0 && base + (size_t)h < n) {
     out[base + h] = a;
-    ok[base + h] = v ? 1 : 0;
+    ok[base + h] = v || id ? 1 : 0;
   }
 }
 
 hipError_t launch_key_validate_wide(hipStream_t st, const uint8_t* pks, size_t n, G1A* out, int* ok) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_key_validate_wide, dim3((unsigned)((n + 1) / 2)), dim3(256), 0, st, pks, n, out, ok);
+  hipLaunchKernelGGL(k_key_validate_wide<false>, dim3((unsigned)((n + 1) / 2)), dim3(256), 0, st, pks, n, out, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_g1_decode_checked_wide(hipStream_t st, const uint8_t* in48, size_t n, G1A* out, int* ok) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_key_validate_wide<true>, dim3((unsigned)((n + 1) / 2)), dim3(256), 0, st, in48, n, out, ok);
   return hipGetLastError();
 }
 

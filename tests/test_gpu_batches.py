@@ -113,6 +113,18 @@ def test_fav_batch_every_item_bad(batch, registry):
     assert not out.any()
 
 
+def test_fav_batch_after_bisection_hashes_its_own_messages(batch, registry):
+    """A host-buffer batch right after a bisected one: its hash must wait for its own message copy (it once forked
+    from the bisection's event, recorded before that copy, and could hash the previous batch's messages)."""
+    for r in range(3):
+        idx, offs, msgs, sigs = _make_batch(batch, 64, 4, seed=60 + r)
+        out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs[96:] + sigs[:96]))
+        assert not out.any()
+        idx, offs, msgs, sigs = _make_batch(batch, 2048, 4, seed=70 + r)
+        out = batch.fast_aggregate_verify_batch(idx, offs, b"".join(msgs), bytes(sigs))
+        assert out.all(), np.nonzero(~out)
+
+
 def test_epoch_shaped_fav_batch(batch, registry):
     """C3 shape at reduced size: a seeded permutation of the registry split into
     slots x committees, one distinct message per (slot, committee)."""

@@ -115,6 +115,42 @@ def test_wide_key_validate_edge_cases():
     assert M._AggregatePKs(pks) == OC.AggregatePKs(pks)
 
 
+def test_pairing_decode_wide_matches_lane_kernel():
+    """The pairing APIs' checked decodes (the wide KeyValidate kernel with the identity accepted, the one-wave signature
+    check) against the lane kernel's checked decode (bls_point_decode, k_pt_decode): each point is paired with the
+    other group's identity, so bls_pairing_check_ex(subgroup) is 1 exactly when the point decodes into its group."""
+    import ctypes
+
+    from bls_mi355x import _native
+    from oracle import bls_oracle_c as OC
+
+    ctx = _native.context()
+    g1s = [b"\xc0" + bytes(47), b"\xe0" + bytes(47), b"\xc0" + bytes(46) + b"\x01", b"\x40" + bytes(47), bytes(48),
+           b"\x80" + bytes(47)]
+    for x in range(1, 16):  # small x: off the curve, or on it and (almost surely) outside G1
+        for flag in (0x80, 0xA0):
+            b = bytearray(x.to_bytes(48, "big"))
+            b[0] |= flag
+            g1s.append(bytes(b))
+    g1s += [OC.SkToPk(k) for k in (1, 2, 0xDEADBEEF)]
+    sig = OC.Sign(77, b"\x42" * 32)
+    g2s = [sig, b"\xc0" + bytes(95), b"\xe0" + bytes(95), b"\xc0" + bytes(94) + b"\x01", bytes(96), b"\x80" + bytes(95),
+           sig[:1] + b"\xff" * 47 + sig[48:], bytes([sig[0] ^ 0x20]) + sig[1:], sig[:95] + bytes([sig[95] ^ 1])]
+
+    def lane_ok(group, pts):
+        ok = (ctypes.c_uint8 * len(pts))()
+        ctx.check(ctx.lib.bls_point_decode(ctx.h, group, b"".join(pts), len(pts), 1, ok))
+        return [bool(v) for v in ok]
+
+    for p, want in zip(g1s, lane_ok(1, g1s)):
+        got = ctx.check(ctx.lib.bls_pairing_check_ex(ctx.h, p, b"\xc0" + bytes(95), 1, 1)) == 1
+        assert got == want, p.hex()
+    for q, want in zip(g2s, lane_ok(2, g2s)):
+        got = ctx.check(ctx.lib.bls_pairing_check_ex(ctx.h, b"\xc0" + bytes(47), q, 1, 1)) == 1
+        assert got == want, q.hex()
+    assert any(lane_ok(1, g1s)) and not all(lane_ok(1, g1s))
+
+
 def test_fe_wide_matches_lane_kernel():
     """The six-wave final-exponentiation check (k_fe_wide, hard part in F2 layout) against the one-wave lane kernel
     and known answers without a pairing: FE(f) = 1 for every f in Fp6 (p^6 - 1 divides (p^12 - 1) / r), so

@@ -31,6 +31,21 @@ def main(reps=int(os.environ.get("REPS", "9"))):
             assert M.AggregateVerify(pks, msgs, sig)
             ts.append(time.perf_counter() - t)
         out[f"av{n}_ms"] = round(statistics.median(ts) * 1e3, 3)
+    # bls_pairing_check_ex of 2 pairs (the KZG verification shape): e(P, Q) e(-P, Q) == 1
+    from bls_mi355x import _native
+    from oracle import bls_oracle as O
+
+    ctx = _native.context()
+    P, Q = O.g1_mul(O.G1_GEN, 12345), O.g2_mul(O.G2_GEN, 678)
+    g1 = O.g1_compress(P) + O.g1_compress(O.g1_neg(P))
+    g2 = O.g2_compress(Q) * 2
+    assert ctx.check(ctx.lib.bls_pairing_check_ex(ctx.h, g1, g2, 2, 1)) == 1
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        ctx.check(ctx.lib.bls_pairing_check_ex(ctx.h, g1, g2, 2, 1))
+        ts.append(time.perf_counter() - t)
+    out["pairing_check2_ms"] = round(statistics.median(ts) * 1e3, 3)
     print(json.dumps(out), flush=True)
 
 
