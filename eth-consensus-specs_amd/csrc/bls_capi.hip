@@ -516,11 +516,11 @@ int bls_device_info(bls_ctx* ctx, char* name, size_t name_len, int* cu_count) {
 //   stream2: hash_to_G2(msg) on one wave (k_h2c_wide)
 //   stream3 (job 0's third stream, or the context's per-call stream when job 0 has two): signature decode + G2
 //            subgroup check (k_sig_validate_wide)
-//   stream1: KeyValidate of every key (+ their sum), then -- after both
-//            branches -- the Miller loops of (apk, H) and (-G1, sigma) fused on
-//            ONE k_miller_wide workgroup, the six-wave final exponentiation
-//            (k_fe_wide) on the same stream, and both verdict words (FE, live)
-//            back in one pinned copy.
+//            then the Miller loop of (-G1, sigma) on one k_miller_wide workgroup (it overlaps the hash's tail)
+//   stream1: KeyValidate of every key (+ their sum), then -- after the hash --
+//            the Miller loop of (apk, H) on another, the six-wave final
+//            exponentiation (k_fe_wide) of both loops' product on the same
+//            stream, and both verdict words (FE, live) back in one pinned copy.
 static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uint8_t* msg, size_t msg_len,
                           const uint8_t* sig96) {
   Job& J = *ctx->j;
@@ -540,12 +540,14 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   d_offs = reinterpret_cast<uint64_t*>(d_in + offs_at);
   SCR(S_G1A, n, keys);
   SCR(S_OK, n + 2, ok);  // key verdicts | sig verdict | live
-  SCR(S_PC_P, 2, P);  // P[0] apk, P[1] -G1 (k_percall_pairs)
+  SCR(S_PC_P, 3, P);  // P[0] apk, P[1] -G1 (k_percall_pairs), P[2] -G1 (the signature's pair, its own stream)
   SCR(S_G2A, 2, Q);
+  Fp2* hz = nullptr;  // H's Jacobian Z (k_h2c_wide skips its inversion; the Miller loop's additions take Q as is)
+  if (!ctx->force_fb) SCR(S_G2A_B, 1, hz);  // (the forced-fallback test hook overwrites H affine after the kernel)
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
   SCR(S_AV_FLAG, 1, flag);
-  SCR(S_F, 3, f);  // f(apk, H) | f(-G1, sigma) | their product
+  SCR(S_F, 2, f);  // f(apk, H) | f(-G1, sigma)
   SCR(S_INT, 4, d_r);
   uint8_t* d_pk = d_in;
   uint8_t* d_sig = d_in + 48 * n;
@@ -572,21 +574,28 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   // one wave of wavefront-cooperative arithmetic for the one message (bls_wide.h); 32-byte messages (every
   // signing root) take the register-resident expand_message_xmd
   const uint64_t* h_offs = msg_len == 32 ? nullptr : d_offs;
-  LK(launch_h2c_wide(st2, 1, d_msg, h_offs, Q, flag));
+  LK(launch_h2c_wide(st2, 1, d_msg, h_offs, Q, flag, hz));
   CK(h2c_fallback(ctx, st2, 1, d_msg, h_offs, flag, Q));
   HIPCK(hipEventRecord(J.ev_join, st2));
   LK(launch_sig_validate_wide(ss, d_sig, 1, Q + 1, ok + n));
   HIPCK(hipEventRecord(J.ev_sig, ss));
+  // (-G1, sigma)'s Miller loop right behind the signature check, beside the hash (constant lines for a rejected
+  // signature): one pair per workgroup, so the critical path after the hash is one pair's loop, not two
+  hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, ss, P + 2);
+  LK(hipGetLastError());
+  LK(launch_miller_wide(ss, P + 2, Q + 1, ok + n, nullptr, 1, f + 1));
+  HIPCK(hipEventRecord(J.ev_msm, ss));
   LK(launch_keys(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
   LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
-  // both pairs' Miller loop on one workgroup: (apk, H) -- rejected inputs are identities there, `live` decides --
-  // and (-G1, sigma), constant lines for a rejected signature
-  LK(launch_miller_wide(st, P, Q, nullptr, ok + n, 2, f + 2));
-  // the six-wave final check on the same stream, then both verdict words in one copy (FE | live) and one sync
-  PROF2(7, st, launch_fe_wide(st, f + 2, 1, d_r));
+  // (apk, H): rejected inputs are identities there, `live` decides
+  LK(launch_miller_wide(st, P, Q, nullptr, nullptr, 1, f, hz));
+  HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
+  // the six-wave final check of f(apk, H) f(-G1, sigma) on the same stream, then both verdict words in one copy
+  // (FE | live) and one sync
+  PROF2(7, st, launch_fe_wide(st, f, 2, d_r));
   hipLaunchKernelGGL(k_copy_int, dim3(1), dim3(64), 0, st, ok + n + 1, d_r + 1);
   LK(hipGetLastError());
   int res[2] = {0, 0};

@@ -116,15 +116,18 @@ hipError_t launch_gt_mul(hipStream_t st, const uint8_t* a, const uint8_t* b, uin
 
 // wavefront-cooperative arithmetic (bls_wide.hip)
 hipError_t launch_wide_selftest(hipStream_t st, size_t nw, const uint8_t* be48, int* bad);
-// hash_to_G2 with one wave per message (msgs 32 B apart when offs is null); flag[i] = 1: recompute on the fallback
-hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag);
+// hash_to_G2 with one wave per message (msgs 32 B apart when offs is null); flag[i] = 1: recompute on the fallback;
+// Hz: H in Jacobian coordinates (Z in Hz, 1 for flagged items) instead of affine
+hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag,
+                           Fp2* Hz = nullptr);
 hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out);
 // signature decode + subgroup check with one wave per signature (k_sig_validate semantics)
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok);
 // the whole Miller loop of npairs <= 2 pairs on one workgroup (line waves + six f waves): out = f (tower Fp12);
-// ok0 / ok1 (nullable): pair 0 / 1 runs with constant lines unless *okp
+// ok0 / ok1 (nullable): pair 0 / 1 runs with constant lines unless *okp; qz (nullable): the pairs' Q are Jacobian
+// (X, Y in Q, Z in qz; the f differs from the affine Q's by an Fp2 factor: the same final exponentiation)
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
-                              Fp12* out);
+                              Fp12* out, const Fp2* qz = nullptr);
 // n pairs on ceil(n / 2) workgroups of the per-call kernel: out[0 .. ceil(n / 2)) (ok per pair, or nullptr)
 hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out);
 // final-exponentiation check of the product of f[0 .. n): easy part lane-parallel, hard part on six waves (F2)

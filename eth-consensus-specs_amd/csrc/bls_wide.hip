@@ -68,11 +68,13 @@ __global__ void __launch_bounds__(64) k_wide_selftest(size_t nw, const uint8_t* 
 // and 3-isogeny of u_0 in half 0 and of u_1 in half 1, their sum, the cofactor clearing
 //   H = [x^2 - x - 1] Q + [x - 1] psi(Q) + psi^2(2 Q)  as  M = [|x|] Q,  A' = M - psi(Q),
 //   C = psi^2(2 Q) - psi(Q) + M - Q,  H = C + [|x|] A'   (A' = -A of k_g2x_pre1t / k_g2x_post1t)
-// in complete projective formulas (F2 layout), and the affine H.  flag[i] = 1 for the cases the fallback
-// recomputes (SSWU `rare`, a vanishing isogeny denominator, an exceptional P0 + P1).
+// in complete projective formulas (F2 layout), and the affine H -- or, Hz != nullptr, H in Jacobian coordinates
+// (X, Y in H[i], Z in Hz[i]: no inversion; the per-call Miller loop takes it as is, and a flagged item gets Z = 1
+// for the fallback's affine point).  flag[i] = 1 for the cases the fallback recomputes (SSWU `rare`, a vanishing
+// isogeny denominator, an exceptional P0 + P1).
 // msgs: 32-byte messages msgs[32 i ..] (offs == nullptr) or msgs[offs[i] .. offs[i+1]).
 __global__ void __launch_bounds__(256) k_h2c_wide(size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H,
-                                                  int* flag) {
+                                                  int* flag, Fp2* Hz) {
   const size_t i = blockIdx.x;
   if (i >= B) return;  // (the whole workgroup)
   __shared__ uint32_t x4[8 * 64];
@@ -104,9 +106,19 @@ __global__ void __launch_bounds__(256) k_h2c_wide(size_t B, const uint8_t* msgs,
   C = p2f_add(K, C, p2f_neg(K, Qp));
   const P2F M2 = p2f_mul_xabs4(K, Ap, x4, w);
   if (w) return;  // waves 1 .. 3: no barrier after the chains
-  const G2A h = p2f_to_aff(K, p2f_add(K, C, M2));
   const int bad = (rare | izero | exc) ? 1 : 0;
   const int bad_any = __builtin_amdgcn_readlane(bad, 0) | __builtin_amdgcn_readlane(bad, 32);
+  if (Hz) {
+    Fp2 z;
+    const G2A h = p2f_to_jac(K, p2f_add(K, C, M2), z);
+    if (threadIdx.x == 0) {
+      H[i] = h;
+      Hz[i] = bad_any ? fp2_one() : z;
+      flag[i] = bad_any;
+    }
+    return;
+  }
+  const G2A h = p2f_to_aff(K, p2f_add(K, C, M2));
   if (threadIdx.x == 0) {
     H[i] = h;
     flag[i] = bad_any;
@@ -281,9 +293,10 @@ hipError_t launch_h2c_wide_dbg(hipStream_t st, const uint8_t* msg32, Fp* out) {
   return hipGetLastError();
 }
 
-hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag) {
+hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const uint64_t* offs, G2A* H, int* flag,
+                           Fp2* Hz) {
   if (!B) return hipSuccess;
-  hipLaunchKernelGGL(k_h2c_wide, dim3((unsigned)B), dim3(256), 0, st, B, msgs, offs, H, flag);
+  hipLaunchKernelGGL(k_h2c_wide, dim3((unsigned)B), dim3(256), 0, st, B, msgs, offs, H, flag, Hz);
   return hipGetLastError();
 }
 
@@ -540,7 +553,10 @@ struct WaveBar {  // barrier of the first nw waves of the workgroup: cnt counts 
 
 struct LineW {
   uint32_t X, Y, Z, xQ, yQ, nxP, yP;
-  __device__ void init(const G1A& P, const G2A& Q, bool live) {
+  // Q in Jacobian coordinates (jac: xQ, yQ are X_Q, Y_Q): Z_Q, Z_Q^2, Z_Q^3, X_Q Z_Q for the additions
+  uint32_t zq, zq2, zq3, xzq;
+  bool jac;
+  __device__ void init(const WKG& K, const G1A& P, const G2A& Q, bool live, const Fp2* qz = nullptr) {
     const G2A q = live ? Q : g2_generator();
     nxP = live ? w_from_fp(fp_neg(P.x)) : 0u;
     yP = live ? w_from_fp(P.y) : 0u;
@@ -548,7 +564,14 @@ struct LineW {
     yQ = wf_from_fp2(q.y);
     X = xQ;
     Y = yQ;
-    Z = wf_from_fp2(fp2_one());
+    jac = live && qz;  // (wave-uniform)
+    Z = wf_from_fp2(jac ? *qz : fp2_one());
+    if (jac) {
+      zq = Z;
+      zq2 = wf_sqr(K.k2048_2, Z);
+      zq3 = wf_mul(K.kneg, zq2, Z);
+      xzq = wf_mul(K.kneg, xQ, Z);
+    }
   }
   // the doubling step on the pair's three line waves (w = 0, 1, 2): dbl's thirteen products in five rounds --
   // {A = X^2, B = Y^2, ZZ = Z^2}, {(Y + Z)^2, C = B^2, F = E^2}, {(X + B)^2, E X, E ZZ}, {z3 ZZ, E (D - x3),
@@ -586,6 +609,7 @@ struct LineW {
   }
   // addition of Q (affine): T = T + Q, the record into o (by the writing wave only, when write)
   __device__ void add(const WKG& K, uint32_t* o, bool write = true) {
+    if (jac) return add_jac(K, o, write);
     const uint32_t kn = K.kneg, ks = K.k2048_2;
     const uint32_t z1z1 = wf_sqr(ks, Z);
     const uint32_t u2 = wf_mul(kn, xQ, z1z1);
@@ -603,6 +627,35 @@ struct LineW {
       o[0] = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
       o[64] = wmul(r, nxP);
       o[128] = wmul(z3, yP);
+    }
+    X = x3;
+    Y = y3;
+    Z = z3;
+  }
+  // addition of a Jacobian Q (add-2007-bl: U1 = X Z_Q^2, S1 = Y Z_Q^3, H = U2 - U1, r = 2 (S2 - S1), Z3 = 2 Z Z_Q H).
+  // The slope is r / Z3, so Z3 Z_Q^3 l(P) = Z3 Z_Q^3 y_P - r Z_Q^3 x_P + (r X_Q Z_Q - Y_Q Z3): the record
+  // (l0, l2, l3) = (r X_Q Z_Q - Y_Q Z3, r Z_Q^3 (-x_P), Z3 Z_Q^3 y_P), the affine record times Z_Q^3 (an Fp2 factor,
+  // which the final exponentiation maps to 1).  Bounds as the affine addition: every subtrahend a product or X < 516p.
+  __device__ void add_jac(const WKG& K, uint32_t* o, bool write) {
+    const uint32_t kn = K.kneg, ks = K.k2048_2;
+    const uint32_t z1z1 = wf_sqr(ks, Z);
+    const uint32_t u1 = wf_mul(kn, X, zq2);
+    const uint32_t u2 = wf_mul(kn, xQ, z1z1);
+    const uint32_t s1 = wf_mul(kn, Y, zq3);
+    const uint32_t s2 = wf_mul(kn, wf_mul(kn, yQ, Z), z1z1);
+    const uint32_t h = wsubk(K.k1, u2, u1);
+    const uint32_t hh = wf_sqr(ks, h);
+    const uint32_t i4 = wmuls<4>(hh);
+    const uint32_t j = wf_mul(kn, h, i4);
+    const uint32_t r = wmuls<2>(wsubk(K.k1, s2, s1));
+    const uint32_t v = wf_mul(kn, u1, i4);
+    const uint32_t x3 = wsubk(K.k1, wf_sqr(ks, r), wadd(j, wmuls<2>(v)));
+    const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, s1, j)));
+    const uint32_t z3 = wf_mul(kn, wmuls<2>(wf_mul(kn, Z, zq)), h);
+    if (write) {
+      o[0] = wsubk(K.k1, wf_mul(kn, r, xzq), wf_mul(kn, yQ, z3));
+      o[64] = wmul(wf_mul(kn, r, zq3), nxP);
+      o[128] = wmul(wf_mul(kn, z3, zq3), yP);
     }
     X = x3;
     Y = y3;
@@ -638,11 +691,13 @@ constexpr int MLF_LW = 3;  // line waves per pair
 __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(const G1A* P, const G2A* Q,
                                                                                const int* ok0, const int* ok1,
                                                                                int npairs, Fp12* out,
-                                                                               const int* okv, int per_block) {
+                                                                               const int* okv, int per_block,
+                                                                               const Fp2* qz) {
   if (per_block) {
     const int b = (int)blockIdx.x;
     P += MLF_PAIRS * b;
     Q += MLF_PAIRS * b;
+    if (qz) qz += MLF_PAIRS * b;
     out += b;
     ok0 = okv ? okv + MLF_PAIRS * b : nullptr;
     ok1 = okv ? okv + MLF_PAIRS * b + 1 : nullptr;
@@ -668,7 +723,7 @@ __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(c
     if (pi >= npairs) return;  // (the whole trio)
     LineW T;
     const int* okp = pi ? ok1 : ok0;
-    T.init(P[pi], Q[pi], (!okp || *okp) && !P[pi].inf && !Q[pi].inf);
+    T.init(K, P[pi], Q[pi], (!okp || *okp) && !P[pi].inf && !Q[pi].inf, qz ? qz + pi : nullptr);
     WaveBar tb{&tbc[pi], 0, MLF_LW};
     int step = 0;
 #pragma unroll 1
@@ -738,10 +793,10 @@ __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(c
 }
 
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
-                              Fp12* out) {
+                              Fp12* out, const Fp2* qz) {
   if (npairs < 1 || npairs > MLF_PAIRS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out,
-                     nullptr, 0);
+                     nullptr, 0, qz);
   return hipGetLastError();
 }
 
@@ -751,7 +806,8 @@ hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, cons
   if (!n) return hipSuccess;
   if (n > (size_t)1 << 20) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_miller_wide, dim3((unsigned)((n + MLF_PAIRS - 1) / MLF_PAIRS)),
-                     dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, nullptr, nullptr, (int)n, out, ok, 1);
+                     dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, nullptr, nullptr, (int)n, out, ok, 1,
+                     (const Fp2*)nullptr);
   return hipGetLastError();
 }
 

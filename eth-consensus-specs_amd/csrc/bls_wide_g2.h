@@ -400,5 +400,13 @@ __device__ __forceinline__ G2A p2f_to_aff(const WKG& K, const P2F& p) {
   return r;
 }
 
+// Jacobian (X Z, Y Z^2, Z) of a projective (X : Y : Z), canonical Fp2 words; z = 0 is the identity (inf set)
+__device__ __forceinline__ G2A p2f_to_jac(const WKG& K, const P2F& p, Fp2& z) {
+  const uint32_t zz = wf_sqr(K.k2048_2, p.z);
+  const Fp2 x = wf_to_fp2(wf_mul(K.kneg, p.x, p.z)), y = wf_to_fp2(wf_mul(K.kneg, p.y, zz));
+  z = wf_to_fp2(p.z);
+  return G2A{x, y, fp2_is_zero(z)};
+}
+
 }  // namespace wide
 }  // namespace bls
