@@ -20,6 +20,7 @@ namespace {
 
 enum Slot {
   S_IN0, S_IN1, S_IN2, S_IN3, S_OFFS, S_G1A, S_G2A, S_G2A_B, S_OK, S_G1J, S_G1J_T, S_G2J, S_G2J_T, S_F, S_F_T, S_INT,
+  S_PC_PZ,
   // FAV batch state (kept between partial and finish)
   S_FAV_F, S_FAV_FT, S_APK, S_STATUS, S_GSTAT, S_APKA, S_SIG, S_RP, S_RS, S_H, S_FPART, S_SEED, S_BYTES, S_FCHK, S_FLAG, S_RSC, S_MSMU, S_MSMF, S_MSTAT, S_HCF, S_RPJ, S_MLINES,
   // bisection fallback (fav_bisect)
@@ -544,6 +545,8 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   SCR(S_G2A, 2, Q);
   Fp2* hz = nullptr;  // H's Jacobian Z (k_h2c_wide skips its inversion; the Miller loop's additions take Q as is)
   if (!ctx->force_fb) SCR(S_G2A_B, 1, hz);  // (the forced-fallback test hook overwrites H affine after the kernel)
+  Fp* pz = nullptr;  // the key sum's Jacobian Z (no inversion; the Miller loop scales its lines by Z^3)
+  if (n > 1) SCR(S_PC_PZ, 1, pz);
   SCR(S_G1J_T, 1024, tmp);
   SCR(S_G1J, 1, apk);
   SCR(S_AV_FLAG, 1, flag);
@@ -588,10 +591,10 @@ static int verify_percall(bls_ctx* ctx, const uint8_t* pks48, size_t n, const ui
   LK(launch_keys(st, d_pk, n, keys, ok));
   if (n > 1) LK(launch_g1_sum_aff(st, keys, nullptr, n, tmp, apk));
   HIPCK(hipStreamWaitEvent(st, J.ev_sig, 0));
-  LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1));
+  LK(launch_percall_pairs(st, keys, ok, n, apk, ok + n, P, ok + n + 1, pz));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
   // (apk, H): rejected inputs are identities there, `live` decides
-  LK(launch_miller_wide(st, P, Q, nullptr, nullptr, 1, f, hz));
+  LK(launch_miller_wide(st, P, Q, nullptr, nullptr, 1, f, hz, pz));
   HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
   // the six-wave final check of f(apk, H) f(-G1, sigma) on the same stream, then both verdict words in one copy
   // (FE | live) and one sync

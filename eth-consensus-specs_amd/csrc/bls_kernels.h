@@ -11,7 +11,7 @@ hipError_t launch_g2_sum_aff(hipStream_t st, const G2A* in, const int* ok, size_
 hipError_t launch_g1_compress(hipStream_t st, const G1J* in, uint8_t* out48, int* is_inf);
 hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96);
 hipError_t launch_percall_pairs(hipStream_t st, const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum,
-                                const int* sig_ok, G1A* P, int* live);
+                                const int* sig_ok, G1A* P, int* live, Fp* pz = nullptr);
 hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst, uint32_t dst_len, G2A* out);
 hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n, uint8_t* out, int* ok);
 hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok);
@@ -126,8 +126,9 @@ hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t 
 // the whole Miller loop of npairs <= 2 pairs on one workgroup (line waves + six f waves): out = f (tower Fp12);
 // ok0 / ok1 (nullable): pair 0 / 1 runs with constant lines unless *okp; qz (nullable): the pairs' Q are Jacobian
 // (X, Y in Q, Z in qz; the f differs from the affine Q's by an Fp2 factor: the same final exponentiation)
+// pz (nullable): the pairs' P are Jacobian (X, Y in P, Z in pz; the lines scaled by Z^3, an Fp factor)
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
-                              Fp12* out, const Fp2* qz = nullptr);
+                              Fp12* out, const Fp2* qz = nullptr, const Fp* pz = nullptr);
 // n pairs on ceil(n / 2) workgroups of the per-call kernel: out[0 .. ceil(n / 2)) (ok per pair, or nullptr)
 hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out);
 // final-exponentiation check of the product of f[0 .. n): easy part lane-parallel, hard part on six waves (F2)

@@ -139,12 +139,24 @@ __global__ void k_g2_compress(const G2J* in, uint8_t* out96) {
 // (apk, H(m)) and (-G1, sigma) for k_miller2_vm.  apk is the validated key
 // (n == 1) or the sum of the validated keys; *live = 0 if any key failed
 // KeyValidate, the sum is the identity, or the signature failed its checks.
+// pz != nullptr: P[0] keeps the sum's Jacobian X, Y and pz[0] its Z (1 for n == 1) -- no inversion; the wide
+// Miller loop scales its lines by Z^3 instead.
 __global__ void k_percall_pairs(const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum, const int* sig_ok,
-                                G1A* P, int* live) {
+                                G1A* P, int* live, Fp* pz) {
   if (threadIdx.x || blockIdx.x) return;
   int ok = sig_ok[0];
   for (size_t i = 0; i < n; i++) ok = ok && key_ok[i];
-  const G1A a = n == 1 ? keys[0] : jac_to_aff(apk_sum[0]);
+  G1A a;
+  if (n == 1) {
+    a = keys[0];
+    if (pz) pz[0] = FP_ONE;
+  } else if (pz) {
+    const G1J& j = apk_sum[0];
+    a = G1A{j.x, j.y, jac_is_inf(j)};
+    pz[0] = j.z;
+  } else {
+    a = jac_to_aff(apk_sum[0]);
+  }
   ok = ok && !a.inf;
   P[0] = a;
   P[1] = g1_neg_generator();
@@ -480,8 +492,8 @@ hipError_t launch_g2_compress(hipStream_t st, const G2J* in, uint8_t* out96) {
   return hipSuccess;
 }
 hipError_t launch_percall_pairs(hipStream_t st, const G1A* keys, const int* key_ok, size_t n, const G1J* apk_sum,
-                                const int* sig_ok, G1A* P, int* live) {
-  LAUNCH(k_percall_pairs, 1, 64, st, keys, key_ok, n, apk_sum, sig_ok, P, live);
+                                const int* sig_ok, G1A* P, int* live, Fp* pz) {
+  LAUNCH(k_percall_pairs, 1, 64, st, keys, key_ok, n, apk_sum, sig_ok, P, live, pz);
   return hipSuccess;
 }
 hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t* offs, size_t n, const uint8_t* dst,

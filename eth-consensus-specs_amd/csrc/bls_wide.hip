@@ -556,10 +556,17 @@ struct LineW {
   // Q in Jacobian coordinates (jac: xQ, yQ are X_Q, Y_Q): Z_Q, Z_Q^2, Z_Q^3, X_Q Z_Q for the additions
   uint32_t zq, zq2, zq3, xzq;
   bool jac;
-  __device__ void init(const WKG& K, const G1A& P, const G2A& Q, bool live, const Fp2* qz = nullptr) {
+  // P in Jacobian coordinates (pz): x_P = X / Z^2, y_P = Y / Z^3, so Z^3 l(P) = Z^3 l0 + l2 (-X Z) + l3 Y: the
+  // P factors -X Z and Y and every record's l0 times zp3 = Z^3 (an Fp factor: the same final exponentiation)
+  uint32_t zp3;
+  bool pjac;
+  __device__ void init(const WKG& K, const G1A& P, const G2A& Q, bool live, const Fp2* qz = nullptr,
+                       const Fp* pz = nullptr) {
     const G2A q = live ? Q : g2_generator();
-    nxP = live ? w_from_fp(fp_neg(P.x)) : 0u;
+    pjac = live && pz;  // (wave-uniform)
+    nxP = live ? w_from_fp(fp_neg(pjac ? fp_mul(P.x, *pz) : P.x)) : 0u;
     yP = live ? w_from_fp(P.y) : 0u;
+    if (pjac) zp3 = w_from_fp(fp_mul(fp_sqr(*pz), *pz));
     xQ = wf_from_fp2(q.x);
     yQ = wf_from_fp2(q.y);
     X = xQ;
@@ -599,7 +606,8 @@ struct LineW {
     tb.sync();
     const uint32_t y3 = wsubk(K.k1, xs[640 + l], wmuls<8>(C));
     if (w == 0) {
-      o[0] = wsubk(K.k1, EX, wmuls<2>(B));
+      const uint32_t l0 = wsubk(K.k1, EX, wmuls<2>(B));
+      o[0] = pjac ? wmul(l0, zp3) : l0;
       o[64] = xs[704 + l];
       o[128] = wmul(xs[576 + l], yP);
     }
@@ -624,7 +632,8 @@ struct LineW {
     const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, Y, j)));
     const uint32_t z3 = wsubk(K.k1, wf_sqr(ks, wadd(Z, h)), wadd(z1z1, hh));
     if (write) {
-      o[0] = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
+      const uint32_t l0 = wsubk(K.k1, wf_mul(kn, r, xQ), wf_mul(kn, yQ, z3));
+      o[0] = pjac ? wmul(l0, zp3) : l0;
       o[64] = wmul(r, nxP);
       o[128] = wmul(z3, yP);
     }
@@ -653,7 +662,8 @@ struct LineW {
     const uint32_t y3 = wsubk(K.k1, wf_mul(kn, r, wsubk(K.k256, v, x3)), wmuls<2>(wf_mul(kn, s1, j)));
     const uint32_t z3 = wf_mul(kn, wmuls<2>(wf_mul(kn, Z, zq)), h);
     if (write) {
-      o[0] = wsubk(K.k1, wf_mul(kn, r, xzq), wf_mul(kn, yQ, z3));
+      const uint32_t l0 = wsubk(K.k1, wf_mul(kn, r, xzq), wf_mul(kn, yQ, z3));
+      o[0] = pjac ? wmul(l0, zp3) : l0;
       o[64] = wmul(wf_mul(kn, r, zq3), nxP);
       o[128] = wmul(wf_mul(kn, z3, zq3), yP);
     }
@@ -692,12 +702,13 @@ __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(c
                                                                                const int* ok0, const int* ok1,
                                                                                int npairs, Fp12* out,
                                                                                const int* okv, int per_block,
-                                                                               const Fp2* qz) {
+                                                                               const Fp2* qz, const Fp* pz) {
   if (per_block) {
     const int b = (int)blockIdx.x;
     P += MLF_PAIRS * b;
     Q += MLF_PAIRS * b;
     if (qz) qz += MLF_PAIRS * b;
+    if (pz) pz += MLF_PAIRS * b;
     out += b;
     ok0 = okv ? okv + MLF_PAIRS * b : nullptr;
     ok1 = okv ? okv + MLF_PAIRS * b + 1 : nullptr;
@@ -723,7 +734,8 @@ __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(c
     if (pi >= npairs) return;  // (the whole trio)
     LineW T;
     const int* okp = pi ? ok1 : ok0;
-    T.init(K, P[pi], Q[pi], (!okp || *okp) && !P[pi].inf && !Q[pi].inf, qz ? qz + pi : nullptr);
+    T.init(K, P[pi], Q[pi], (!okp || *okp) && !P[pi].inf && !Q[pi].inf, qz ? qz + pi : nullptr,
+           pz ? pz + pi : nullptr);
     WaveBar tb{&tbc[pi], 0, MLF_LW};
     int step = 0;
 #pragma unroll 1
@@ -793,10 +805,10 @@ __global__ void __launch_bounds__(64 * (6 + MLF_LW * MLF_PAIRS)) k_miller_wide(c
 }
 
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
-                              Fp12* out, const Fp2* qz) {
+                              Fp12* out, const Fp2* qz, const Fp* pz) {
   if (npairs < 1 || npairs > MLF_PAIRS) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_miller_wide, dim3(1), dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, ok0, ok1, npairs, out,
-                     nullptr, 0, qz);
+                     nullptr, 0, qz, pz);
   return hipGetLastError();
 }
 
@@ -807,7 +819,7 @@ hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, cons
   if (n > (size_t)1 << 20) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_miller_wide, dim3((unsigned)((n + MLF_PAIRS - 1) / MLF_PAIRS)),
                      dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, nullptr, nullptr, (int)n, out, ok, 1,
-                     (const Fp2*)nullptr);
+                     (const Fp2*)nullptr, (const Fp*)nullptr);
   return hipGetLastError();
 }
 
