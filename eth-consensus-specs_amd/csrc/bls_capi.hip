@@ -201,10 +201,12 @@ static const size_t WIDE_H2C_MAX = getenv("BLS_WIDE_H2C_MAX") ? (size_t)atol(get
 // ms, (1,024) 7.95 -> 7.31; at 8,192 pairs the wave programs' throughput wins); *nf = the number of f values written;
 // knob BLS_WIDE_MILLER_MAX
 static const size_t WIDE_MILLER_MAX = getenv("BLS_WIDE_MILLER_MAX") ? (size_t)atol(getenv("BLS_WIDE_MILLER_MAX")) : 1100;
-static hipError_t launch_miller_call(hipStream_t st, const G1A* P, const G2A* Q, size_t n, Fp12* f, size_t* nf) {
+// qz: Jacobian Z of every Q (the wide kernel only: callers pass it only when n <= WIDE_MILLER_MAX)
+static hipError_t launch_miller_call(hipStream_t st, const G1A* P, const G2A* Q, size_t n, Fp12* f, size_t* nf,
+                                     const Fp2* qz = nullptr) {
   if (n <= WIDE_MILLER_MAX) {
     *nf = (n + 1) / 2;
-    return launch_miller_wide_n(st, P, Q, nullptr, n, f);
+    return launch_miller_wide_n(st, P, Q, nullptr, n, f, qz);
   }
   *nf = n;
   return launch_miller_wave(st, P, Q, nullptr, n, f);
@@ -371,6 +373,11 @@ __global__ void k_set_neg_g1(G1A* p) {
   G1A g = g1_generator();
   g.y = fp_neg(g.y);
   *p = g;
+}
+
+__global__ void k_set_fp2_one(Fp2* z) {
+  if (threadIdx.x || blockIdx.x) return;
+  *z = fp2_one();
 }
 
 }  // namespace
@@ -656,6 +663,10 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   SCR(S_FPART, 1, fo);
   SCR(S_AV_HCF, h2c_scratch_fd(n), d_hf);
   SCR(S_AV_FLAG, n, d_flag);
+  // the hashes in Jacobian coordinates when both the hash and the Miller loop take the wide kernels (no inversion
+  // per message; Z of the signature's pair 1); not under the forced-fallback test hook (it rewrites H affine)
+  Fp2* hz = nullptr;
+  if (n <= WIDE_H2C_MAX && n + 1 <= WIDE_MILLER_MAX && !ctx->force_fb) SCR(S_G2A_B, n + 1, hz);
   CK(h2d(ctx, d_sig, sig96, 96));
   CK(h2d(ctx, d_msgs, msgs, offs[n]));
   CK(h2d(ctx, d_offs, offs.data(), (n + 1) * sizeof(uint64_t)));
@@ -664,11 +675,15 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   HIPCK(hipStreamWaitEvent(st2, J.ev_fork, 0));
   if (ss != st) HIPCK(hipStreamWaitEvent(ss, J.ev_fork, 0));
   LK(launch_sig_validate_wide(ss, d_sig, 1, Q + n, d_w));
+  if (hz) {
+    hipLaunchKernelGGL(k_set_fp2_one, dim3(1), dim3(64), 0, ss, hz + n);
+    LK(hipGetLastError());
+  }
   HIPCK(hipEventRecord(J.ev_sig, ss));
   bool m32 = true;  // all signing roots: the FAV batches' 32-byte h2c kernels (msgs are then 32 B apart)
   for (size_t i = 0; i < n && m32; i++) m32 = msg_lens[i] == 32;
   if (n <= WIDE_H2C_MAX)  // up to ~a thousand messages: one wide workgroup each, lower latency than the lane chains
-    LK(launch_h2c_wide(st2, n, d_msgs, m32 ? nullptr : d_offs, Q, d_flag));
+    LK(launch_h2c_wide(st2, n, d_msgs, m32 ? nullptr : d_offs, Q, d_flag, hz));
   else if (m32)
     LK(launch_h2c(st2, n, d_msgs, nullptr, d_hf, Q, d_flag));
   else
@@ -688,7 +703,7 @@ int bls_aggregate_verify(bls_ctx* ctx, const uint8_t* pks48, size_t n, const uin
   hipLaunchKernelGGL(k_set_neg_g1, dim3(1), dim3(64), 0, st, P + n);
   LK(hipGetLastError());
   size_t nf = 0;
-  LK(launch_miller_call(st, P, Q, n + 1, f, &nf));  // a rejected signature: constant lines there
+  LK(launch_miller_call(st, P, Q, n + 1, f, &nf, hz));  // a rejected signature: constant lines there
   LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
   PROF2(7, st, launch_fe_wide(st, fo, 1, d_w + 1));
   int w[2] = {0, 0};

@@ -130,7 +130,8 @@ hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t 
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
                               Fp12* out, const Fp2* qz = nullptr, const Fp* pz = nullptr);
 // n pairs on ceil(n / 2) workgroups of the per-call kernel: out[0 .. ceil(n / 2)) (ok per pair, or nullptr)
-hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out);
+hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out,
+                                const Fp2* qz = nullptr);
 // final-exponentiation check of the product of f[0 .. n): easy part lane-parallel, hard part on six waves (F2)
 hipError_t launch_fe_wide(hipStream_t st, const Fp12* f, int n, int* out, uint64_t* ts = nullptr);  // ts: stage clocks (tests)
 // KeyValidate with two keys per wave (k_key_validate semantics)

@@ -814,12 +814,13 @@ hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const 
 
 // n pairs on ceil(n / 2) workgroups of k_miller_wide (one f per workgroup, out[0 .. (n + 1) / 2)): the latency of
 // one wide Miller loop for a few hundred pairs, where the lane kernels' chains take ~2 ms whatever n
-hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out) {
+hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out,
+                                const Fp2* qz) {
   if (!n) return hipSuccess;
   if (n > (size_t)1 << 20) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_miller_wide, dim3((unsigned)((n + MLF_PAIRS - 1) / MLF_PAIRS)),
                      dim3(64 * (6 + MLF_LW * MLF_PAIRS)), 0, st, P, Q, nullptr, nullptr, (int)n, out, ok, 1,
-                     (const Fp2*)nullptr, (const Fp*)nullptr);
+                     qz, (const Fp*)nullptr);
   return hipGetLastError();
 }
 
