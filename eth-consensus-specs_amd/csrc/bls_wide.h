@@ -238,6 +238,53 @@ __device__ __forceinline__ uint32_t wswap(uint32_t v) {
   return whalf() ? (uint32_t)sw[0] : (uint32_t)sw[1];
 }
 
+// a^e on two waves of a workgroup whose waves all call it (it holds two workgroup barriers): wave 0 forms the
+// squarings a^(2^i) and hands each to wave 1 through an LDS ring of PW_RING slots, wave 1 multiplies in those of
+// the set bits of e (LSB first) -- the chain is the nbits - 1 squarings alone, not the squarings plus a window
+// method's products (sswu's (p - 3) / 4: 378 squarings, 228 set bits).  ring: PW_RING x 64 words of LDS, cnt: two
+// ints of LDS (squarings published, ring slots released); every wave returns a^e.
+constexpr int PW_RING = 32;
+__device__ __forceinline__ uint32_t wpow_2w(uint32_t a, const uint32_t* e, int nbits, uint32_t* ring, int* cnt,
+                                            int w) {
+  const int l = wlane();
+  if (threadIdx.x == 0) {
+    cnt[0] = 0;
+    cnt[1] = 0;
+  }
+  __syncthreads();
+  if (w == 0) {  // the squarer: slot i % PW_RING <- a^(2^i), once wave 1 has released index i - PW_RING
+    uint32_t sq = a;
+#pragma unroll 1
+    for (int i = 0; i < nbits; ++i) {
+      if (i >= PW_RING)
+        while (__hip_atomic_load(&cnt[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i - PW_RING)
+          __builtin_amdgcn_s_sleep(1);
+      ring[(i % PW_RING) * 64 + l] = sq;
+      if (l == 0) __hip_atomic_store(&cnt[0], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (i + 1 < nbits) sq = wsqr(sq);
+    }
+  } else if (w == 1) {  // the multiplier: r = prod of a^(2^i) over the set bits i
+    uint32_t r = 0;
+    bool started = false;
+#pragma unroll 1
+    for (int i = 0; i < nbits; ++i) {
+      if (!((e[i >> 5] >> (i & 31)) & 1u)) continue;
+      if (l == 0) __hip_atomic_store(&cnt[1], i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // below i: done
+      while (__hip_atomic_load(&cnt[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= i)
+        __builtin_amdgcn_s_sleep(1);
+      const uint32_t v = ring[(i % PW_RING) * 64 + l];
+      r = started ? wmul(r, v) : v;
+      started = true;
+      if (l == 0) __hip_atomic_store(&cnt[1], i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    ring[l] = r;  // every slot is released: the squarer is done with the ring
+  }
+  __syncthreads();
+  const uint32_t r = ring[l];
+  __syncthreads();  // (the ring is free again for the caller's next use)
+  return r;
+}
+
 // a^e for a fixed exponent (little-endian u32 limbs, bit nbits-1 set), sliding window w = 3 (as fq_pow_w3)
 __device__ __forceinline__ uint32_t wpow(uint32_t a, const uint32_t* e, int nbits) {
   const uint32_t a2 = wsqr(a);

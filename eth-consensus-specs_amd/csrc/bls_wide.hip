@@ -78,6 +78,8 @@ __global__ void __launch_bounds__(256) k_h2c_wide(size_t B, const uint8_t* msgs,
   const size_t i = blockIdx.x;
   if (i >= B) return;  // (the whole workgroup)
   __shared__ uint32_t x4[8 * 64];
+  __shared__ uint32_t pring[PW_RING * 64];  // the SSWU exponentiations' squaring ring (wpow_2w)
+  __shared__ int pcnt[2];
   const int w = (int)(threadIdx.x >> 6);  // four waves: the same work up to the cofactor chains' doublings
   const WKG K = wkg_init();
   Fp2 u[2];
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(256) k_h2c_wide(size_t B, const uint8_t* msgs,
   const Fp2 uh{fp_select(hi, u[1].c0, u[0].c0), fp_select(hi, u[1].c1, u[0].c1)};
   W2 x, y;
   bool rare = false, izero = false, exc = false;
-  sswu_w(K, uh, x, y, rare);
+  sswu_w(K, uh, x, y, rare, pring, pcnt, w);
   const J2W P = iso_w(K, x, y, izero);
   const J2W Po{w2swap(P.x), w2swap(P.y), w2swap(P.z)};
   // Q = P0 + P1 (W2 layout, both halves), then the cofactor chains in F2 layout on half 0's Q

@@ -134,7 +134,9 @@ __device__ __forceinline__ int w2_sgn0(W2 a) { return fp2_sgn0_lane(w2_to_fp2(a)
 // RFC 9380 simplified SWU on E2' (bls_lane.h map_to_curve_sswu_lane_i, step for step): one exponentiation before
 // the final square root; `rare` marks g(x1) = 0 and g(x) in Fp (the caller's item goes to k_h2c_fallback).
 // Subtrahends are products or sums of two (< 4.0002p) against 64p; every product operand stays below ~70p.
-__device__ __forceinline__ void sswu_w(const WKG& K, const Fp2& u_lane, W2& x, W2& y, bool& rare) {
+// ring / cnt / wv (all or none): the two exponentiations on two waves (wpow_2w; every wave of the workgroup calls)
+__device__ __forceinline__ void sswu_w(const WKG& K, const Fp2& u_lane, W2& x, W2& y, bool& rare,
+                                       uint32_t* ring = nullptr, int* cnt = nullptr, int wv = 0) {
   const WK K1 = wk_of(K);
   const int sgn_u = fp2_sgn0_lane(u_lane);
   const W2 u = w2_from_fp2(u_lane);
@@ -158,7 +160,8 @@ __device__ __forceinline__ void sswu_w(const WKG& K, const Fp2& u_lane, W2& x, W
   const W2 xnc = w2mul(K1, w2conj(K1, xd), xn);  // the conjugate (< 66p) as the first factor: 64p - b1 needs b1 < 62p
   const uint32_t agd4 = wmul(ag, d4), agd = wmul(ag, d);
   const bool ag0 = w_is_zero(ag);
-  const uint32_t z = wpow(w, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+  const uint32_t z = ring ? wpow_2w(w, EXP_SQRT_M3, EXP_SQRT_M3_BITS, ring, cnt, wv)
+                          : wpow(w, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
   const uint32_t z2 = wsqr(z);
   const bool square = ag0 | w_is_one(wmul(z2, w));
   const uint32_t dinv0 = wmul(z2, agd4), dinvn = wneg(K1, dinv0);
@@ -174,7 +177,8 @@ __device__ __forceinline__ void sswu_w(const WKG& K, const Fp2& u_lane, W2& x, W
   // square root of gx from the root n of its norm (bls_lane.h fp2_sqrt_from_norm_root)
   const uint32_t inv2 = w_from_fp(FP_INV2);
   const uint32_t t = wmul(wadd(gx.c0, n), inv2);
-  const uint32_t sr = wpow(t, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+  const uint32_t sr = ring ? wpow_2w(t, EXP_SQRT_M3, EXP_SQRT_M3_BITS, ring, cnt, wv)
+                           : wpow(t, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
   const uint32_t ts = wmul(t, sr);
   const uint32_t hs = wmul(wmul(gx.c1, inv2), sr);
   const bool tsq = w_is_one(wmul(ts, sr));
