@@ -308,9 +308,13 @@ hipError_t launch_h2c_wide(hipStream_t st, size_t B, const uint8_t* msgs, const 
 // by the norm square root (bls_lane.h fp2_sqrt_lane_i; the pure-Fp case, unreachable for x of a valid point with
 // probability ~2^-381, runs fp2_sqrt_lane_i on the lanes -- a wave-uniform branch), the sign, and
 // psi(sigma) == -[|x|] sigma through the wide Jacobian chain (an exceptional addition means a small order: reject).
-__global__ void __launch_bounds__(64) k_sig_validate_wide(const uint8_t* sigs96, size_t n, G2A* out, int* ok) {
+// Two waves: wave 1 only multiplies in the square roots' exponentiations (wpow_2w) and otherwise repeats wave 0.
+__global__ void __launch_bounds__(128) k_sig_validate_wide(const uint8_t* sigs96, size_t n, G2A* out, int* ok) {
   const size_t i = blockIdx.x;
-  if (i >= n) return;
+  if (i >= n) return;  // (the whole workgroup)
+  __shared__ uint32_t pring[PW_RING * 64];
+  __shared__ int pcnt[2];
+  const int wv = (int)(threadIdx.x >> 6);
   const WKG K = wkg_init();
   const WK K1 = wk_of(K);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(sigs96 + 96 * i);
@@ -341,11 +345,11 @@ __global__ void __launch_bounds__(64) k_sig_validate_wide(const uint8_t* sigs96,
         y = w2_from_fp2(yl);
       } else {
         const uint32_t nrm = wadd(wsqr(rhs.c0), wsqr(rhs.c1));
-        const uint32_t nr = wpow(nrm, EXP_SQRT, EXP_SQRT_BITS);
+        const uint32_t nr = wpow_2w(nrm, EXP_SQRT, EXP_SQRT_BITS, pring, pcnt, wv);
         on = w_eq(K1, wsqr(nr), nrm);
         const uint32_t inv2 = w_from_fp(FP_INV2);
         const uint32_t t = wmul(wadd(rhs.c0, nr), inv2);
-        const uint32_t sr = wpow(t, EXP_SQRT_M3, EXP_SQRT_M3_BITS);
+        const uint32_t sr = wpow_2w(t, EXP_SQRT_M3, EXP_SQRT_M3_BITS, pring, pcnt, wv);
         const uint32_t ts = wmul(t, sr), hs = wmul(wmul(rhs.c1, inv2), sr);
         const bool tsq = w_is_one(wmul(ts, sr));
         const uint32_t nts = wneg(K1, ts);
@@ -381,7 +385,7 @@ __global__ void __launch_bounds__(64) k_sig_validate_wide(const uint8_t* sigs96,
 
 hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t n, G2A* out, int* ok) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_validate_wide, dim3((unsigned)n), dim3(64), 0, st, sigs, n, out, ok);
+  hipLaunchKernelGGL(k_sig_validate_wide, dim3((unsigned)n), dim3(128), 0, st, sigs, n, out, ok);
   return hipGetLastError();
 }
 
