@@ -77,14 +77,30 @@ SINGLE_KERNEL = ("miller", "miller_lines", "fav_gather")
 # fused kernel (k_miller_fused: G2 lines and f accumulation in one workgroup, lines in LDS; bls_capi.hip)
 MILLER_FUSED = os.environ.get("BLS_MILLER_FUSED") == "1"
 MSM_PAIRS = 64  # the MSM's bit-sum pairs (-2^b G1, U_b) join every batch's Miller loops (bls_msm.hip)
-# lanes per item of the lane kernels (full register file, one wave per SIMD): k_miller_acc4<2> four lanes per two
-# pairs (bls_miller_pair.hip), k_miller_lines2 two per pair (bls_miller_lane.hip), k_sig_lane2 one for the G1
-# chain and two for the G2 chain of an item (bls_chain_lane.hip)
-LANE_KERNELS = {"miller": 3 if MILLER_FUSED else 2, "miller_lines": 2, "sig_vm": 3}
+# pairs per f of k_miller_acc4q<G> on batches of >= ACC_SHARED_MIN items (bls_capi.hip fav_prepare: BLS_ACC_G, default
+# 4), one pair per f below
+ACC_G = {"1": 1, "2": 2}.get(os.environ.get("BLS_ACC_G", "4"), 4)
+ACC_SHARED_MIN = int(os.environ.get("BLS_ACC_SHARED_MIN", "4096"))
+
+
+def acc_g(items: int) -> int:
+    return ACC_G if items >= ACC_SHARED_MIN else 1
+
+
+def lane_kernels(items: int) -> dict:
+    """Lanes per item of the lane kernels (full register file, one wave per SIMD): k_miller_acc4q<G> four lanes per
+    G pairs (bls_miller_pair.hip), k_miller_lines2 two per pair (bls_miller_lane.hip), k_sig_lane2 one for the G1
+    chain and two for the G2 chain of an item (bls_chain_lane.hip)."""
+    return {"miller": 3 if MILLER_FUSED else 4 / acc_g(items), "miller_lines": 2, "sig_vm": 3}
+
+
 GATHER_BYTES_PER_KEY = 4 + 96  # u32 index + one 96-B registry record (affine x, y; validity in x's top bit)
-# profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)
-KERNEL_SYMBOL = {"miller": "k_miller_fused<2>" if MILLER_FUSED else "k_miller_acc4q<2>", "miller_lines": "k_miller_lines2",
-                 "fav_gather": "k_fav_gather_q<16>"}
+
+
+def kernel_symbol(kernel: str, items: int) -> str | None:
+    """profile entry -> kernel symbol in the rocprofv3 summaries (profiles/*kernel_stats*.md)."""
+    return {"miller": "k_miller_fused<2>" if MILLER_FUSED else f"k_miller_acc4q<{acc_g(items)}>",
+            "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}.get(kernel)
 ROCPROF_AVG = os.path.join(ROOT, "profiles", "rocprof_kernel_avg.json")
 LIB = os.path.join(ROOT, "eth-consensus-specs_amd", "libblsmi355x.so")
 
@@ -100,12 +116,13 @@ C4_TOTAL, C4_CHUNK = 10 ** 6, 125_000
 def launch_grid(kernel: str, items: int) -> int | None:
     """Threads of one launch of the roofline kernel over `items` FAV items (rocprofv3's grid_x).  The Miller
     kernels run items + 64 pairs (the MSM's bit-sum pairs): k_miller_fused<2> one 192-thread workgroup per 64 pairs,
-    k_miller_acc4q<2> 4 lanes per two pairs in 64-lane workgroups, k_miller_lines2 2 lanes per pair;
+    k_miller_acc4q<G> 4 lanes per G pairs in 64-lane workgroups, k_miller_lines2 2 lanes per pair;
     k_fav_gather_q<16> 16 lanes per aggregate (bls_miller_pair.hip, bls_miller_lane.hip, bls_kernels.hip)."""
     np_ = items + MSM_PAIRS
     if kernel == "miller" and MILLER_FUSED:
         return (np_ + 63) // 64 * 192
-    lanes = {"miller": 4 * ((np_ + 1) // 2), "miller_lines": 2 * np_, "fav_gather": 16 * items}.get(kernel)
+    g = acc_g(items)
+    lanes = {"miller": 4 * ((np_ + g - 1) // g), "miller_lines": 2 * np_, "fav_gather": 16 * items}.get(kernel)
     return None if lanes is None else (lanes + 63) // 64 * 64
 
 
@@ -117,9 +134,11 @@ def model_fme(n: int):
         "sig_vm": 1200 + 1000 + 400,    # G2 subgroup check, RLC G1, RLC G2 (MSM share)
         "fav_hash": 6600,
         # Miller loop, 4400 FME per pair: all of it in the fused kernel, or split between the two kernels of
-        # the split form in proportion to the products each executes per pair: k_miller_acc4<2> (f shared by two
-        # pairs: 62 Fp12 squarings x 36 / 2 + 68 sparse line products x 43 = 4040) and k_miller_lines2 (T: 63
-        # doublings x 26 + 5 additions x 35 = 1813).  (The MSM's 64 extra pairs per batch are not counted.)
+        # the split form in the proportion of the products each executes per pair with f shared by two pairs
+        # (k_miller_acc4q: 62 Fp12 squarings x 36 / 2 + 68 sparse line products x 43 = 4040; k_miller_lines2, T:
+        # 63 doublings x 26 + 5 additions x 35 = 1813).  The share is the model's, fixed whatever G the shipped
+        # kernel runs (with four pairs per f it executes 62 x 36 / 4 + 68 x 43 = 3,482 FME per pair).  (The MSM's 64
+        # extra pairs per batch are not counted.)
         "miller": 4400 if MILLER_FUSED else 4400 * 4040 / 5853,
         "miller_lines": 4400 * 1813 / 5853,
     }
@@ -492,9 +511,85 @@ def _lib_sha() -> str | None:
         return None
 
 
+def rank_envs(n: int, port: int, base: dict | None = None) -> list[dict]:
+    """The environment of each of the n rank processes the launcher starts (what torch.distributed.run sets for
+    one node: RANK = LOCAL_RANK = r, WORLD_SIZE = n, the rendezvous at 127.0.0.1:port)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpus() -> int:
+    """GPUs this process may use, counted WITHOUT initialising HIP (torch.cuda.device_count() reads the device
+    list only on this image; no kernel, stream or context is created in the launcher process)."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def launch_ranks(n: int, argv: list[str], dry_run: bool = False) -> int:
+    """--gpus N > 1 started as a plain `python bench.py --gpus N` (no WORLD_SIZE in the environment): start one
+    child process per GPU, each re-running this script with the same arguments and the rank environment of
+    rank_envs(), and return the first non-zero child exit code (the other ranks are then terminated, so no rank
+    waits in a collective for a dead peer).  Nothing here touches the GPU: the children initialise HIP, one GPU
+    each (BLSMI355X_DEVICE = LOCAL_RANK).  dry_run prints the plan (one JSON line) and starts nothing."""
+    import subprocess
+
+    port = _free_port()
+    envs = rank_envs(n, port)
+    cmd = [sys.executable, os.path.abspath(__file__), *argv]
+    if dry_run:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        print(json.dumps({"launcher": {"ranks": n, "cmd": cmd,
+                                       "children": [{k: e[k] for k in keys} for e in envs]}}), flush=True)
+        return 0
+    have = visible_gpus()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs on this node but {have} are visible "
+              f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')!r}); refusing to run fewer ranks "
+              f"than asked", file=sys.stderr, flush=True)
+        return 2
+    procs = {r: subprocess.Popen(cmd, env=e) for r, e in enumerate(envs)}
+    rc = 0
+    try:
+        while procs:
+            for r, p in list(procs.items()):
+                code = p.poll()
+                if code is None:
+                    continue
+                del procs[r]
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code  # a signal -s -> 128 + s, as a shell reports it
+                    print(f"bench.py launcher: rank {r} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in procs.values():
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for q in procs.values():  # left only if the launcher itself was interrupted
+            q.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; N > 1 without WORLD_SIZE starts one rank process per GPU")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="print the rank processes --gpus N would start (environments) and exit")
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2")
     ap.add_argument("--steps", type=int, default=40, help="timed steps (4 in flight: fewer passes under-fill the pipeline)")
     ap.add_argument("--warmup", type=int, default=2)
@@ -519,6 +614,16 @@ def main():
     ap.add_argument("--no-percall", action="store_true", help="skip the drop-in per-call latency figures")
     ap.add_argument("--no-parity", action="store_true", help="skip the parity sample")
     args = ap.parse_args()
+
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} (set by the launcher) but --gpus {args.gpus}; the line would "
+              f"report a world the run does not have", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if env_world is None and (args.gpus > 1 or args.launch_dry_run):
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], dry_run=args.launch_dry_run))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -695,7 +800,7 @@ def main():
                 traffic, tsrc = tj["bytes_per_dispatch"].get(dom), tj["source"]
         except (OSError, ValueError, KeyError):
             pass
-        roof = {"bound": "valu-int", "kernel": dom, "symbol": KERNEL_SYMBOL.get(dom), "achieved": round(ach, 4),
+        roof = {"bound": "valu-int", "kernel": dom, "symbol": kernel_symbol(dom, per_launch), "achieved": round(ach, 4),
                 "peak": round(PEAK_INT_OPS / 1e12, 2), "unit": "Tops/s", "frac": round(ach / (PEAK_INT_OPS / 1e12), 5),
                 "frac_source": f"this run: algorithmic ops / hipEvent launch time ({args.roofline_passes} "
                                f"one-batch-at-a-time passes after the timed region)",
@@ -707,7 +812,7 @@ def main():
             with open(ROCPROF_AVG) as fh:
                 rj = json.load(fh)
             grid = launch_grid(dom, per_launch)
-            ent = rj.get("avg_ms_by_grid", {}).get(KERNEL_SYMBOL.get(dom), {}).get(str(grid))
+            ent = rj.get("avg_ms_by_grid", {}).get(kernel_symbol(dom, per_launch), {}).get(str(grid))
             if ent and rj.get("lib_sha256_16") and rj["lib_sha256_16"] == _lib_sha():
                 r_ms = ent["avg_ms"]
                 roof["rocprof_avg_ms"] = r_ms
@@ -718,8 +823,9 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
         roof["frac_of_measured_mad_rate"] = round(roof["achieved"] * 1e12 / MEASURED_MAD_OPS, 5)
-        if dom in LANE_KERNELS:  # k lanes per item, one wave per SIMD: the launch holds ceil(k B / 64) SIMDs
-            occ = min(1.0, ((LANE_KERNELS[dom] * per_launch + 63) // 64) / (cus * 4))
+        lk = lane_kernels(per_launch)
+        if dom in lk:  # k lanes per item, one wave per SIMD: the launch holds ceil(k B / 64) SIMDs
+            occ = min(1.0, ((int(lk[dom] * per_launch) + 63) // 64) / (cus * 4))
             roof["occupied_simd_frac"] = round(occ, 4)
             roof["frac_of_occupied_simds"] = round(roof["frac"] / occ, 4)
     # secondary figure: algorithmic HBM bytes of the registry gather per launch / its duration

@@ -66,24 +66,41 @@ def shard_bounds_by_work(offsets, rank: int, world: int, per_item: int = ITEM_WO
     offsets[i + 1] - offsets[i] (per_item = 0: pure pubkey count).  Rank r's block starts at the aggregate whose
     cumulative work is nearest r / world of the total, so every rank's share is within one aggregate's work of
     total / world; uniform committees give shard_bounds' blocks.  Every rank computes the same cut points from
-    the same offsets (no exchange)."""
+    the same offsets (no exchange).
+
+    No rank's block is empty when B >= world: the cut points are made strictly increasing (a heavily skewed
+    committee, e.g. one of 131,072 keys after a thousand of one, would otherwise leave the ranks between two cuts
+    with nothing, and a rank with no aggregates cannot take part in a job).  Only B < world leaves ranks empty;
+    those submit an empty shard, whose partial is the identity, so they still join every all-gather
+    (bls_fav_job_submit_dev with B = 0)."""
+    cuts = work_cuts(offsets, world, per_item)
+    return cuts[rank], cuts[rank + 1]
+
+
+def work_cuts(offsets, world: int, per_item: int = ITEM_WORK_KEYS) -> list[int]:
+    """The world + 1 cut points of shard_bounds_by_work: 0 = c_0 <= c_1 <= ... <= c_world = B, strictly increasing
+    when B >= world."""
     offs = np.asarray(offsets, dtype=np.int64)
     B = int(offs.size) - 1
     if B <= 0:
-        return 0, 0
+        return [0] * (world + 1)
     cum = offs - offs[0] + per_item * np.arange(B + 1, dtype=np.int64)  # work before aggregate i
     total = int(cum[-1])
 
     def cut(r: int) -> int:
-        if r <= 0:
-            return 0
-        if r >= world:
-            return B
         t = total * r / world
         i = int(np.searchsorted(cum, t))  # first boundary with work >= t
         if i > 0 and (i > B or t - cum[i - 1] <= cum[i] - t):
             i -= 1
         return min(max(i, 0), B)
 
-    lo, hi = cut(rank), cut(rank + 1)
-    return lo, max(lo, hi)
+    c = [0] + [cut(r) for r in range(1, world)] + [B]
+    if B >= world:  # every block non-empty: c_r >= c_{r-1} + 1 going up, then c_r <= c_{r+1} - 1 going down
+        for r in range(1, world):
+            c[r] = max(c[r], c[r - 1] + 1)
+        for r in range(world - 1, 0, -1):
+            c[r] = min(c[r], c[r + 1] - 1)
+    else:
+        for r in range(1, world):
+            c[r] = max(c[r], c[r - 1])
+    return c

@@ -38,6 +38,7 @@ enum Slot {
   // partial and finish calls, and fav_bisect reads them back)
   S_PC_P,
   S_OWN,  // the job's own final check (job_submit)
+  S_COMM, S_CV,  // the all-gathered partials of all ranks and their check's verdict (enqueue_comm_check)
   NSLOT
 };
 
@@ -76,6 +77,11 @@ struct Job {
   hipEvent_t ev_own = nullptr;
   bool own_pending = false;
   int own_state = -1;
+  // multi-GPU (a communicator on the context): job_submit enqueues the all-gather of the partial on the context's
+  // comm stream (ev_comm: gathered) and the product's check on the job's stream; h_own[1] = that verdict once
+  // ev_cv has passed.  The own check then runs only when the combined check fails (read_own).
+  bool comm_pending = false;
+  hipEvent_t ev_comm = nullptr, ev_cv = nullptr;
   int fav_mg = 1;  // pairs per f of the prepared batch's Miller accumulation
   // last bisection fallback: final-exponentiation checks and rounds (levels); the checks of a FAV bisection are
   // counted on the device (bis_dev_checks, read after the job's stream by bls_last_fallback_stats)
@@ -101,6 +107,9 @@ struct bls_ctx {
   // the per-call API's signature branch (verify_percall, AggregateVerify) beside the hash on stream2 and the keys
   // on stream1 when job 0 has two streams: one more stream, used by no batch
   hipStream_t pc_stream = nullptr;
+  // the FAV jobs' all-gathers (multi-GPU): ONE stream, so the collectives run in the order the jobs were submitted
+  // -- the same order on every rank -- whichever job's product is ready first
+  hipStream_t comm_stream = nullptr;
   // registry (HBM resident): RegKey records of 96 B of affine (x, y) padded to 128 B and 128-B aligned (one
   // cache line per random read), validity in x's top bit; 128 MiB per 2^20 keys, 256 MiB for 2^21
   RegKey* reg = nullptr;
@@ -201,13 +210,15 @@ static const size_t WIDE_H2C_MAX = getenv("BLS_WIDE_H2C_MAX") ? (size_t)atol(get
 // ms, (1,024) 7.95 -> 7.31; at 8,192 pairs the wave programs' throughput wins); *nf = the number of f values written;
 // knob BLS_WIDE_MILLER_MAX
 static const size_t WIDE_MILLER_MAX = getenv("BLS_WIDE_MILLER_MAX") ? (size_t)atol(getenv("BLS_WIDE_MILLER_MAX")) : 1100;
-// qz: Jacobian Z of every Q (the wide kernel only: callers pass it only when n <= WIDE_MILLER_MAX)
+// qz: Jacobian Z of every Q, which only the wide kernel takes: a call with qz beyond WIDE_MILLER_MAX is refused
+// (the wave-program kernel would read Jacobian X, Y as affine coordinates)
 static hipError_t launch_miller_call(hipStream_t st, const G1A* P, const G2A* Q, size_t n, Fp12* f, size_t* nf,
                                      const Fp2* qz = nullptr) {
   if (n <= WIDE_MILLER_MAX) {
-    *nf = (n + 1) / 2;
+    *nf = miller_wide_nf(n);
     return launch_miller_wide_n(st, P, Q, nullptr, n, f, qz);
   }
+  if (qz) return hipErrorInvalidValue;
   *nf = n;
   return launch_miller_wave(st, P, Q, nullptr, n, f);
 }
@@ -427,6 +438,8 @@ static bool job_init(Job& J, int prio_hi, int streams) {
          hipEventCreateWithFlags(&J.ev_fe, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_bis, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&J.ev_own, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_comm, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&J.ev_cv, hipEventDisableTiming) == hipSuccess &&
          hipHostMalloc((void**)&J.h_own, 2 * sizeof(int), hipHostMallocDefault) == hipSuccess &&
          hipHostMalloc((void**)&J.h_partial, 576, hipHostMallocDefault) == hipSuccess;
 }
@@ -437,8 +450,8 @@ static void job_destroy(Job& J) {
     if (s) (void)hipStreamSynchronize(s);
   for (auto& b : J.buf)
     if (b.p) (void)hipFree(b.p);
-  hipEvent_t es[11] = {J.ev_fork,    J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial,
-                       J.ev_h2c, J.ev_fb,   J.ev_fe,  J.ev_bis, J.ev_own};
+  hipEvent_t es[13] = {J.ev_fork, J.ev_join, J.ev_sig, J.ev_msm, J.ev_gather, J.ev_partial, J.ev_h2c,
+                       J.ev_fb,   J.ev_fe,   J.ev_bis, J.ev_own, J.ev_comm,   J.ev_cv};
   for (hipEvent_t e : es)
     if (e) (void)hipEventDestroy(e);
   if (J.h_partial) (void)hipHostFree(J.h_partial);
@@ -477,6 +490,7 @@ int bls_ctx_create(int device, bls_ctx** out) {
   const bool fe_job = !(fev && !strcmp(fev, "ctx"));
   if (hipStreamCreateWithFlags(&c->fb_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pc_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking) != hipSuccess ||
       (!fe_job && hipStreamCreateWithPriority(&c->fe_stream, hipStreamNonBlocking, prio_hi) != hipSuccess)) {
     bls_ctx_destroy(c);
     return BLS_E_DEVICE;
@@ -490,7 +504,7 @@ void bls_ctx_destroy(bls_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (Job& J : ctx->jobs) job_destroy(J);
-  for (hipStream_t s : {ctx->fb_stream, ctx->fe_stream, ctx->pc_stream})
+  for (hipStream_t s : {ctx->fb_stream, ctx->fe_stream, ctx->pc_stream, ctx->comm_stream})
     if (s) {
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);
@@ -501,6 +515,7 @@ void bls_ctx_destroy(bls_ctx* ctx) {
     (void)hipEventDestroy(p.second);
   }
   if (ctx->reg) (void)hipFree(ctx->reg);
+  if (ctx->comb) (void)hipFree(ctx->comb);
   if (ctx->force_fb) (void)hipFree(ctx->force_fb);
   if (ctx->pc_stage) (void)hipHostFree(ctx->pc_stage);
   delete ctx;
@@ -1208,10 +1223,21 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   Job& J = *ctx->j;
   hipStream_t st = J.stream, st2 = J.stream2, st3 = J.stream3;
   if (!ctx->comb) {  // the -G1 comb (bls_bisect.hip): the MSM pairs' -2^b G1 and the bisection's -r_i G1
-    HIPCK(hipMalloc(&ctx->comb, neg_g1_comb_entries() * sizeof(G1A)));
-    LK(launch_neg_g1_comb_table(st, ctx->comb));
-    HIPCK(hipStreamSynchronize(st));
+    G1A* tab = nullptr;
+    HIPCK(hipMalloc(&tab, neg_g1_comb_entries() * sizeof(G1A)));
+    hipError_t e = launch_neg_g1_comb_table(st, tab);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {  // never keep a table whose build did not complete
+      (void)hipFree(tab);
+      return fail(ctx, e, "launch_neg_g1_comb_table");
+    }
+    ctx->comb = tab;
   }
+  // the job's own-product verdict belongs to the batch job_submit prepares; any other batch prepared on this slot
+  // (the host-buffer calls on job 0) invalidates it
+  J.own_pending = false;
+  J.own_state = -1;
+  J.comm_pending = false;
   // a two-stream job (stream3 == stream2, BLS_JOB_STREAMS=2, the default): the decode and the MSM run on stream1
   // around the gather, off the hash -> lines chain of stream2
   const bool two = st3 == st2;
@@ -1262,10 +1288,12 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   PROF(10, launch_sig_vm(st, B, gstat, status, dstat, apka, sig, rsc, rpj, rP));
   HIPCK(hipStreamWaitEvent(st, J.ev_join, 0));
   if (fused && !two) HIPCK(hipStreamWaitEvent(st, J.ev_msm, 0));
-  // two pairs share each f (one squaring per step for both) on full batches; below ACC_SHARED_MIN items the
-  // launch under-fills the chip and the chain latency is what counts, so one pair per f (a step is a squaring
-  // and ONE line: ~37 % shorter chains for ~24 % more products)
-  static const int acc_g = getenv("BLS_ACC_G") ? atoi(getenv("BLS_ACC_G")) : 2;  // pairs per f of full batches
+  // four pairs share each f (one squaring per step for all four) on full batches: the least work per pair, and
+  // the pipeline is bound by work (C2 +3.0 % over two pairs per f, profiles/r06a_g4_ab.txt, although the launch
+  // fills only 0.15 of the SIMDs); below ACC_SHARED_MIN items the launch under-fills the chip and the chain latency
+  // is what counts, so one pair per f (a step is a squaring and ONE line: ~37 % shorter chains for ~24 % more
+  // products).  Knob BLS_ACC_G = 1 / 2 / 4.
+  static const int acc_g = getenv("BLS_ACC_G") ? atoi(getenv("BLS_ACC_G")) : 4;  // pairs per f of full batches
   static const size_t shared_min = getenv("BLS_ACC_SHARED_MIN") ? (size_t)atol(getenv("BLS_ACC_SHARED_MIN"))
                                                                 : ACC_SHARED_MIN;
   const int mg = B >= shared_min ? (acc_g == 4 ? 4 : (acc_g == 1 ? 1 : 2)) : 1;
@@ -1382,6 +1410,7 @@ static int fav_finish(bls_ctx* ctx, int batch_ok, bool root_bad, uint8_t* d_out)
     return BLS_E_ARG;
   }
   size_t B = ctx->j->fav_B;
+  if (!B) return 0;  // an empty shard (job_submit with the device exchange): no verdicts
   int* status = (int*)ctx->j->buf[S_STATUS].p;
   if (batch_ok) {
     ctx->j->bis_checks = ctx->j->bis_rounds = 0;
@@ -1947,18 +1976,73 @@ int bls_sync(bls_ctx* ctx) {
 }
 
 // ---------------------------------------------- pipelined FAV batches --
+static int nccl_fail(bls_ctx* c, ncclResult_t r, const char* where);  // multi-GPU exchange, below
+static void comm_fail_abort(bls_ctx* ctx);
+__global__ void k_fp12_set_one(Fp12* f) {
+  if (threadIdx.x || blockIdx.x) return;
+  *f = fp12_one();
+}
+
+// The device-side exchange of a submitted job (multi-GPU, a communicator on the context), enqueued at submit: the
+// comm stream waits for the partial, all-gathers the world's 576-byte partials (the collectives of all jobs on one
+// stream, in submission order -- every rank submits the same jobs in the same order, so the collectives match),
+// and the job's stream multiplies them inside the final-exponentiation kernel and copies the 4-byte verdict to
+// h_own[1] (ev_cv).  No host step between a job's product and its verdict.
+static int enqueue_comm_check(bls_ctx* ctx) {
+  Job& J = *ctx->j;
+  const int W = ctx->comm_world;
+  uint8_t* d_all;
+  Fp12* fw;
+  int* d_cv;
+  SCR(S_COMM, 576 * (size_t)W, d_all);
+  SCR(S_FCHK, W, fw);
+  SCR(S_CV, 1, d_cv);
+  HIPCK(hipStreamWaitEvent(ctx->comm_stream, J.ev_partial, 0));
+  const ncclResult_t r = ncclAllGather(J.buf[S_BYTES].p, d_all, 576, ncclUint8, ctx->comm, ctx->comm_stream);
+  if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllGather");
+  HIPCK(hipEventRecord(J.ev_comm, ctx->comm_stream));
+  HIPCK(hipStreamWaitEvent(J.stream, J.ev_comm, 0));
+  PROF(9, launch_fp12_from_bytes(J.stream, d_all, W, fw));
+  PROF(7, launch_final_check_wave(J.stream, fw, W, d_cv));
+  HIPCK(hipMemcpyAsync(J.h_own + 1, d_cv, sizeof(int), hipMemcpyDeviceToHost, J.stream));
+  HIPCK(hipEventRecord(J.ev_cv, J.stream));
+  J.comm_pending = true;
+  return 0;
+}
+
+// exchange: the job API with a communicator on the context (bls_fav_job_submit_dev) -- the all-gather and the
+// combined check go on the device here and the job's own check is left for a failing combined check (read_own);
+// otherwise (one GPU, or the host-exchange API bls_fav_batch_partial_dev) the own check is enqueued right behind the
+// product.  B == 0 (a rank whose shard is empty) is allowed only with the exchange: its partial is the identity, so
+// the rank still joins every all-gather and its peers never wait for it.
 static int job_submit(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B, const uint8_t* d_msgs32,
-                      const uint8_t* d_sigs96, const uint8_t* seed32) {
-  if (!d_offsets || !d_msgs32 || !d_sigs96 || !seed32 || !B) return BLS_E_ARG;
+                      const uint8_t* d_sigs96, const uint8_t* seed32, bool exchange) {
+  exchange = exchange && ctx->comm;
+  if (!seed32 || (B && (!d_offsets || !d_msgs32 || !d_sigs96)) || (!B && !exchange)) return BLS_E_ARG;
+  Job& J = *ctx->j;
   Fp12* f;
-  CK(fav_prepare(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32, &f));
+  if (B) {
+    CK(fav_prepare(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32, &f));
+  } else {
+    SCR(S_FPART, 1, f);
+    hipLaunchKernelGGL(k_fp12_set_one, dim3(1), dim3(64), 0, J.stream, f);
+    LK(hipGetLastError());
+    J.fav_B = 0;
+    J.fav_ready = true;
+    J.comm_pending = false;
+  }
   uint8_t* d_b;
   SCR(S_BYTES, 576, d_b);
-  Job& J = *ctx->j;
   LK(launch_fp12_to_bytes(J.stream, f, d_b));
   HIPCK(hipMemcpyAsync(J.h_partial, d_b, 576, hipMemcpyDeviceToHost, J.stream));
   HIPCK(hipEventRecord(J.ev_partial, J.stream));
   J.partial_pending = true;
+  if (exchange) {
+    CK(enqueue_comm_check(ctx));
+    J.own_pending = false;
+    J.own_state = B ? -2 : 1;  // -2: computed on demand (read_own); an empty shard passes
+    return 1;
+  }
   // this job's own check, right behind its product on its stream: a single-GPU caller reads it with
   // bls_fav_job_check_own (no host round trip of the partial), and a multi-GPU failure is localised by it
   int* d_own;
@@ -1971,9 +2055,19 @@ static int job_submit(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_off
   return 1;
 }
 
-// *state = the job's own verdict (1 / 0; waits for the check job_submit enqueued).  Returns 0 or BLS_E_*.
+// *state = the job's own verdict (1 / 0): waits for the check job_submit enqueued or, after a submit with the
+// device exchange, runs it now (a failing combined check is the only reader).  Returns 0 or BLS_E_* (no verdict:
+// no batch submitted on this job, or another batch prepared on the slot since).
 static int read_own(bls_ctx* ctx, int* state) {
   Job& J = *ctx->j;
+  if (J.own_state == -2) {
+    int* d_own;
+    SCR(S_OWN, 1, d_own);
+    PROF(7, launch_final_check_wave(J.stream, (const Fp12*)J.buf[S_FPART].p, 1, d_own));
+    HIPCK(hipMemcpyAsync(J.h_own, d_own, sizeof(int), hipMemcpyDeviceToHost, J.stream));
+    HIPCK(hipEventRecord(J.ev_own, J.stream));
+    J.own_pending = true;
+  }
   if (J.own_pending) {
     HIPCK(hipEventSynchronize(J.ev_own));
     J.own_state = J.h_own[0] ? 1 : 0;
@@ -2021,9 +2115,13 @@ static int job_check(bls_ctx* ctx, const uint8_t* partials576, size_t n) {
 // Verdicts are written on the job's stream: a failing batch's bisection runs there without a host round trip, so
 // the caller can check the next job meanwhile (bls_sync / bls_d2h wait for every job stream).
 static int job_finish(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
-  if (!d_out) return BLS_E_ARG;
+  if (!d_out && ctx->j->fav_B) return BLS_E_ARG;
   bool root_bad = false;
-  if (!batch_ok) {  // a failed product of several shards (or of given partials): this job's own check decides
+  Job& J = *ctx->j;
+  // a failed product of several shards (or of given partials): this job's own check decides.  Without a verdict
+  // of its own (another batch was prepared on the slot since its submit) the bisection starts at the root, whose
+  // check it runs first.
+  if (!batch_ok && (J.own_pending || J.own_state != -1)) {
     int own = 0;
     CK(read_own(ctx, &own));
     if (own == 1) batch_ok = 1;  // its own product passes: the failure is elsewhere, every status stands
@@ -2038,7 +2136,7 @@ int bls_fav_batch_partial_dev(bls_ctx* ctx, const uint32_t* d_idx, const uint64_
                               uint8_t* partial576) {
   API_ENTER(ctx);
   if (!partial576) return BLS_E_ARG;
-  const int r = job_submit(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32);
+  const int r = job_submit(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32, false);
   if (r < 0) return r;
   return job_partial(ctx, partial576);
 }
@@ -2056,7 +2154,11 @@ int bls_fav_batch_finish_dev(bls_ctx* ctx, int batch_ok, uint8_t* d_out) {
 int bls_fav_job_submit_dev(bls_ctx* ctx, int job, const uint32_t* d_idx, const uint64_t* d_offsets, size_t B,
                            const uint8_t* d_msgs32, const uint8_t* d_sigs96, const uint8_t* seed32) {
   JOB_ENTER(ctx, job);
-  return job_submit(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32);
+  const int r = job_submit(ctx, d_idx, d_offsets, B, d_msgs32, d_sigs96, seed32, true);
+  // with a communicator, a rank that fails here never enqueues the all-gather its peers are (or will be) in:
+  // abort, so their collectives fail instead of hanging (comm_fail_abort)
+  if (r < 0 && ctx->comm) comm_fail_abort(ctx);
+  return r;
 }
 
 int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576) {
@@ -2125,6 +2227,7 @@ int bls_comm_init(bls_ctx* ctx, const uint8_t* uid128, int rank, int world) {
 int bls_comm_destroy(bls_ctx* ctx) {
   API_ENTER(ctx);
   if (ctx->comm) {
+    HIPCK(hipStreamSynchronize(ctx->comm_stream));  // every all-gather enqueued by a submit has run
     const ncclResult_t r = ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
     if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclCommDestroy");
@@ -2134,11 +2237,6 @@ int bls_comm_destroy(bls_ctx* ctx) {
   return 0;
 }
 
-// All-gather job `job`'s device-resident partial (written by its submit) with
-// every rank's, on the job's stream, then the product's final exponentiation:
-// 1 / 0.  The host never sees the partials.  Every rank must call this for the
-// same jobs in the same order (one outstanding collective at a time: the call
-// waits for the verdict).
 static int comm_abort_locked(bls_ctx* ctx) {
   if (ctx->comm) {
     (void)ncclCommAbort(ctx->comm);
@@ -2154,23 +2252,33 @@ int bls_comm_abort(bls_ctx* ctx) {
   return comm_abort_locked(ctx);
 }
 
+// any error on the exchange path -- a local one included (this rank then skips an all-gather its peers are in)
+// -- leaves the peers waiting in this or a later all-gather: abort so their collectives fail instead of hanging.
+// The first failure's text stays in ctx->err and is repeated by every later call on this context.
+static void comm_fail_abort(bls_ctx* ctx) {
+  ctx->comm_abort_cause = ctx->err;
+  comm_abort_locked(ctx);
+  ctx->err = "RCCL communicator aborted: " + ctx->comm_abort_cause;
+}
+
+// The verdict of job `job`'s combined check: its partial all-gathered with every rank's and the product
+// final-exponentiated, both enqueued by its submit (enqueue_comm_check), so this only waits for the 4-byte
+// verdict: 1 / 0.  The host never sees the partials.  Every rank submits the same jobs in the same order.
 static int job_check_comm(bls_ctx* ctx) {
   Job& J = *ctx->j;
+  if (J.comm_pending) {  // enqueued by job_submit: only the verdict is left to read
+    HIPCK(hipEventSynchronize(J.ev_cv));
+    J.comm_pending = false;
+    J.partial_pending = false;
+    return J.h_own[1] ? 1 : 0;
+  }
   if (!J.partial_pending || !J.buf[S_BYTES].p) {
     ctx->err = "no submitted FAV batch on this job";
     return BLS_E_ARG;
   }
-  const int W = ctx->comm_world;
-  uint8_t* d_all;
-  Fp12* f;
-  SCR(S_IN0, 576 * (size_t)W, d_all);
-  SCR(S_FCHK, W, f);
-  const ncclResult_t r =
-      ncclAllGather(J.buf[S_BYTES].p, d_all, 576, ncclUint8, ctx->comm, J.stream);
-  if (r != ncclSuccess) return nccl_fail(ctx, r, "ncclAllGather");
-  J.partial_pending = false;  // consumed on the device (the pinned host copy is not waited for)
-  PROF(9, launch_fp12_from_bytes(J.stream, d_all, W, f));
-  return run_final_check(ctx, f, W);
+  // a job submitted before the communicator existed: the exchange now (every rank must do the same)
+  CK(enqueue_comm_check(ctx));
+  return job_check_comm(ctx);
 }
 
 int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
@@ -2182,14 +2290,7 @@ int bls_fav_job_check_comm(bls_ctx* ctx, int job) {
     return BLS_E_ARG;
   }
   const int r = job_check_comm(ctx);
-  // any error here -- a local one included (this rank then skips the all-gather its peers are in) -- leaves
-  // the peers waiting in this or a later all-gather: abort so their collectives fail instead of hanging.  The
-  // first failure's text stays in ctx->err and is repeated by every later call on this context.
-  if (r < 0) {
-    ctx->comm_abort_cause = ctx->err;
-    comm_abort_locked(ctx);
-    ctx->err = "RCCL communicator aborted: " + ctx->comm_abort_cause;
-  }
+  if (r < 0) comm_fail_abort(ctx);
   return r;
 }
 

@@ -129,7 +129,9 @@ hipError_t launch_sig_validate_wide(hipStream_t st, const uint8_t* sigs, size_t 
 // pz (nullable): the pairs' P are Jacobian (X, Y in P, Z in pz; the lines scaled by Z^3, an Fp factor)
 hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const int* ok0, const int* ok1, int npairs,
                               Fp12* out, const Fp2* qz = nullptr, const Fp* pz = nullptr);
-// n pairs on ceil(n / 2) workgroups of the per-call kernel: out[0 .. ceil(n / 2)) (ok per pair, or nullptr)
+// n pairs on miller_wide_nf(n) = ceil(n / 2) workgroups of the per-call kernel: out[0 .. miller_wide_nf(n)) (ok per
+// pair, or nullptr)
+size_t miller_wide_nf(size_t n);
 hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out,
                                 const Fp2* qz = nullptr);
 // final-exponentiation check of the product of f[0 .. n): easy part lane-parallel, hard part on six waves (F2)

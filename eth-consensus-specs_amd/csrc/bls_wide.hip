@@ -820,6 +820,8 @@ hipError_t launch_miller_wide(hipStream_t st, const G1A* P, const G2A* Q, const 
 
 // n pairs on ceil(n / 2) workgroups of k_miller_wide (one f per workgroup, out[0 .. (n + 1) / 2)): the latency of
 // one wide Miller loop for a few hundred pairs, where the lane kernels' chains take ~2 ms whatever n
+size_t miller_wide_nf(size_t n) { return (n + MLF_PAIRS - 1) / MLF_PAIRS; }
+
 hipError_t launch_miller_wide_n(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* out,
                                 const Fp2* qz) {
   if (!n) return hipSuccess;

@@ -245,29 +245,39 @@ int bls_fav_job_partial(bls_ctx* ctx, int job, uint8_t* partial576);
 int bls_fav_job_check(bls_ctx* ctx, int job, const uint8_t* partials576, size_t n);
 /* check_own: the final exponentiation of the job's own product alone, which
  * submit already enqueued on the job's stream (the single-GPU check: no host
- * round trip of the partial): 1 / 0.  A finish after a failed multi-shard
- * check uses the same verdict -- a job whose own product passes keeps every
- * per-item status, one whose own product fails bisects below its root. */
+ * round trip of the partial; with a communicator it runs on demand): 1 / 0.
+ * A finish after a failed multi-shard check uses the same verdict -- a job
+ * whose own product passes keeps every per-item status, one whose own product
+ * fails bisects below its root.  Another batch prepared on the job since its
+ * submit (the host-buffer calls use job 0) voids that verdict: check_own is
+ * then BLS_E_ARG and a failing finish bisects from the root. */
 int bls_fav_job_check_own(bls_ctx* ctx, int job);
 int bls_fav_job_finish_dev(bls_ctx* ctx, int job, int batch_ok, uint8_t* d_out);
 
 /* ---- multi-GPU exchange over RCCL ----------------------
  * One communicator per context.  bls_comm_unique_id runs on one rank; its 128
  * bytes reach the other ranks out of band (bench.py: the torchrun TCP store).
- * bls_fav_job_check_comm replaces job_partial + host exchange + job_check: the
- * job's 576-byte partial is all-gathered on the device (ncclAllGather over
- * xGMI, on the job's stream), the world partials are multiplied inside the
- * final-exponentiation kernel, and the verdict (1 / 0) returns.  Every rank
- * calls it for the same jobs in the same order.  A failing verdict is then
- * localised by bls_fav_job_finish_dev(..., 0, ...) on every rank: each
- * re-checks its own partial first, so only the bad shard bisects. */
+ * With a communicator on the context, bls_fav_job_submit_dev itself enqueues
+ * the exchange behind the job's Miller product: the 576-byte partial is
+ * all-gathered on the device (ncclAllGather over xGMI, on the context's one
+ * comm stream, so the collectives run in submission order -- every rank
+ * submits the same jobs in the same order) and the job's stream multiplies
+ * the world partials inside the final-exponentiation kernel.  No host step
+ * sits between a job's product and its verdict; bls_fav_job_check_comm only
+ * waits for that verdict (1 / 0).  The job's own check is then not enqueued:
+ * a failing verdict is localised by bls_fav_job_finish_dev(..., 0, ...) on
+ * every rank, which checks its own partial first, so only the bad shard
+ * bisects.  A rank with an empty shard submits B = 0 (its partial is the
+ * identity) and still joins every all-gather; B = 0 without a communicator is
+ * BLS_E_ARG.  A submit that fails after the communicator exists aborts it
+ * (below), so peers never wait for this rank's collective. */
 int bls_comm_unique_id(uint8_t* out128);
 int bls_comm_init(bls_ctx* ctx, const uint8_t* uid128, int rank, int world);
 int bls_comm_destroy(bls_ctx* ctx);
 int bls_fav_job_check_comm(bls_ctx* ctx, int job);
 /* Abort the communicator (ncclCommAbort): peers blocked in a collective with
  * this rank fail instead of hanging.  The library calls it itself when
- * bls_fav_job_check_comm fails after the communicator exists; a host that
+ * bls_fav_job_submit_dev or bls_fav_job_check_comm fails after the communicator exists; a host that
  * leaves the exchange on its own error (bench.py, dist.py) calls it before
  * exiting.  No-op without a communicator. */
 int bls_comm_abort(bls_ctx* ctx);

@@ -40,6 +40,48 @@ def test_adversarial_plan_every_kind():
     assert {k: list(plan.values()).count(k) for k in bench.BAD_KINDS} == {k: 8 for k in bench.BAD_KINDS}
 
 
+def _run_bench(args, **env_over):
+    import os
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_over)
+    return subprocess.run([sys.executable, bench.__file__, *args], env=env, capture_output=True, text=True,
+                          timeout=300)
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_launcher_dry_run_rank_envs(n):
+    """`python bench.py --gpus N` (no WORLD_SIZE) starts one process per GPU; the dry run prints what each child
+    would get and stops before anything touches HIP."""
+    import json
+
+    p = _run_bench(["--gpus", str(n), "--steps", "3", "--launch-dry-run"])
+    assert p.returncode == 0, p.stderr
+    plan = json.loads(p.stdout.strip().splitlines()[-1])["launcher"]
+    assert plan["ranks"] == n and plan["cmd"][-5:] == ["--gpus", str(n), "--steps", "3", "--launch-dry-run"]
+    ch = plan["children"]
+    assert [c["RANK"] for c in ch] == [str(r) for r in range(n)] == [c["LOCAL_RANK"] for c in ch]
+    assert {c["WORLD_SIZE"] for c in ch} == {str(n)} and {c["MASTER_ADDR"] for c in ch} == {"127.0.0.1"}
+    assert len({c["MASTER_PORT"] for c in ch}) == 1 and int(ch[0]["MASTER_PORT"]) > 0
+
+
+def test_launcher_refuses_world_mismatch_and_missing_gpus():
+    p = _run_bench(["--gpus", "2"], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr and "--gpus 2" in p.stderr
+    # this container has no GPU (the one-GPU box has 1): --gpus 2 must fail loudly, never run one rank and print
+    # n_gpus 1
+    p = _run_bench(["--gpus", "2", "--no-cpu"])
+    assert p.returncode != 0 and "needs 2 GPUs" in p.stderr and '"n_gpus"' not in p.stdout
+
+
+def test_rank_envs():
+    envs = bench.rank_envs(4, 12345, base={"PATH": "/bin", "WORLD_SIZE": "9"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"] and all(e["WORLD_SIZE"] == "4" for e in envs)
+    assert all(e["PATH"] == "/bin" and e["MASTER_PORT"] == "12345" for e in envs)
+
+
 def test_corrupt_kinds():
     B = 4
     sigs = bytearray(bytes(range(96)) * B)

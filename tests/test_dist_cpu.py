@@ -122,6 +122,29 @@ def test_shard_bounds_by_work_balances_variable_committees():
     assert max(naive_work) > 4 * min(naive_work)
 
 
+def test_shard_bounds_by_work_no_empty_rank():
+    """with skewed committees the nearest-cut rule put several cuts on the same aggregate (ranks 1..6
+    of [1] * 1000 + [131072] at world 8 got (1000, 1000)), and an empty shard cannot submit a job.  Every block is
+    non-empty when B >= world; below that the empty ranks are the tail of a partition that still covers B."""
+    import numpy as np
+
+    from bls_mi355x.dist import ITEM_WORK_KEYS, shard_bounds_by_work, work_cuts
+
+    for sizes in ([1] * 1000 + [131072], [131072] + [1] * 1000, [1] * 3 + [131072] * 2 + [1] * 3,
+                  ELECTRA_SIZES, [5] * 8, [7] * 9):
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        for world in (2, 3, 4, 8):
+            for per_item in (0, ITEM_WORK_KEYS):
+                bounds = [shard_bounds_by_work(offs, r, world, per_item) for r in range(world)]
+                _check_partition(bounds, offs, per_item, world)
+                assert all(hi > lo for lo, hi in bounds), (sizes[:4], world, per_item, bounds)
+    for B in range(0, 8):  # fewer aggregates than ranks: a partition of B, non-decreasing cuts
+        offs = np.arange(B + 1) * 512
+        c = work_cuts(offs, 8)
+        assert c[0] == 0 and c[-1] == B and all(a <= b for a, b in zip(c, c[1:]))
+        assert sum(c[r + 1] - c[r] for r in range(8)) == B
+
+
 def _balance_worker(rank, world, port, q):
     import numpy as np
     import torch.distributed as dist

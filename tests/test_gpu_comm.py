@@ -54,6 +54,63 @@ def test_rccl_world1_pipeline():
         dist.destroy_comm(ctx)
 
 
+def test_rccl_empty_shard_joins_the_exchange():
+    """A rank with no aggregates (B < world) submits an empty job: its partial is the identity and it still takes
+    part in the submit-time all-gather (bls_fav_job_submit_dev with B = 0, device exchange only)."""
+    import ctypes
+
+    from bls_mi355x import _native, batch, dist
+
+    ctx = _native.context()
+    batch.Registry(ctx).generate(1 << 10, first_sk=1)
+    offs = batch.DeviceBuffer(ctx, np.zeros(1, dtype=np.uint64))
+    seed = os.urandom(32)
+    # no communicator: an empty job is an argument error
+    assert ctx.lib.bls_fav_job_submit_dev(ctx.h, 1, None, offs.ptr, 0, None, None, seed) == -1
+    dist.init_comm(ctx, 0, 1, DictStore())
+    try:
+        assert ctx.lib.bls_fav_job_submit_dev(ctx.h, 1, None, offs.ptr, 0, None, None, seed) == 1
+        part = ctypes.create_string_buffer(576)
+        assert ctx.lib.bls_fav_job_partial(ctx.h, 1, part) == 1
+        one = bytearray(576)
+        one[47] = 1  # Fp12 one: c0 of the w^0 coefficient (big-endian 48-byte words, c0 then c1 per w-power)
+        assert part.raw == bytes(one)
+        assert ctx.lib.bls_fav_job_check_comm(ctx.h, 1) == 1
+        assert ctx.lib.bls_fav_job_finish_dev(ctx.h, 1, 1, None) == 1
+        # a real batch on the same job afterwards
+        idx, offs2, msgs, sigs = _inputs(batch, 40, 8, 1 << 10, seed=5)
+        rb = batch.ResidentFavBatch(idx, offs2, msgs, bytes(sigs), ctx=ctx)
+        assert rb.run_pipelined([os.urandom(32) for _ in range(3)], comm=True) == [True] * 3 and rb.verdicts().all()
+        rb.free()
+    finally:
+        dist.destroy_comm(ctx)
+        offs.free()
+
+
+def test_finish_after_interleaved_host_batch_bisects_from_root():
+    """a job slot's own verdict belongs to the batch its submit prepared.  A host-buffer batch on job 0
+    in between (bls_fav_batch_indexed) replaces the slot's batch state, so bls_fav_batch_finish_dev(0) must
+    bisect that batch from the root instead of reusing the earlier batch's passing verdict."""
+    from bls_mi355x import _native, batch
+
+    ctx = _native.context()
+    batch.Registry(ctx).generate(1 << 10, first_sk=1)
+    idx, offs, msgs, sigs = _inputs(batch, 30, 8, 1 << 10, seed=6)
+    rb = batch.ResidentFavBatch(idx, offs, msgs, bytes(sigs), ctx=ctx)
+    rb.submit(0, os.urandom(32))
+    assert rb.job_check_own(0)  # the valid device batch passes (its own verdict: 1)
+    bad = bytearray(sigs)
+    bad[96 * 4: 96 * 5] = bad[96 * 5: 96 * 6]  # item 4 signs another message
+    host = batch.fast_aggregate_verify_batch(idx, offs, msgs, bytes(bad), ctx=ctx)  # job 0's state is now this batch
+    assert not host[4] and host.sum() == 29
+    out = batch.DeviceBuffer(ctx, nbytes=30)
+    ctx.check(ctx.lib.bls_fav_batch_finish_dev(ctx.h, 0, out.ptr))
+    v = out.to_host().astype(bool)
+    assert not v[4] and v.sum() == 29, v
+    out.free()
+    rb.free()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
