@@ -38,6 +38,7 @@ enum Slot {
   // partial and finish calls, and fav_bisect reads them back)
   S_PC_P,
   S_OWN,  // the job's own final check (job_submit)
+  S_GAFF, S_GREDO,  // the affine gather's level lists and redo flags (bls_gather_aff.hip)
   S_COMM, S_CV,  // the all-gathered partials of all ranks and their check's verdict (enqueue_comm_check)
   NSLOT
 };
@@ -1264,7 +1265,23 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   CK(h2c_fallback(ctx, st2, B, d_msgs, nullptr, flag, H));
   PROF2(1, sd, launch_sig_decode(sd, B, d_msgs, d_sigs, d_seed, sig, rsc, dstat));
   HIPCK(hipEventRecord(J.ev_sig, sd));
-  PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, (uint32_t)ctx->reg_n, apka, gstat));
+  // the registry gather: the complete-formula kernel (k_fav_gather_q, 108 registers: four waves per SIMD, beside the
+  // one-wave lane kernels whose register files it fits into), or with BLS_GATHER=affine (read per batch) affine
+  // additions sharing one inversion per level (bls_gather_aff.hip: 42 % fewer VALU instructions per aggregate, but
+  // 234 registers, so it holds its SIMDs alone or in pairs; C2 measured the same within +-1 % over three A/Bs,
+  // profiles/r06_gather_ab.txt); aggregates with an exceptional pair are redone by the complete formulas
+  const char* gv = getenv("BLS_GATHER");
+  const size_t gw = (gv && !strcmp(gv, "affine")) ? fav_gather_aff_words(B) : 0;
+  if (gw) {
+    uint32_t* gscr;
+    int* redo;
+    SCR(S_GAFF, gw, gscr);
+    SCR(S_GREDO, B, redo);
+    PROF(0, launch_fav_gather_aff(st, d_idx, d_offs, B, ctx->reg, (uint32_t)ctx->reg_n, apka, gstat, gscr, redo));
+    LK(launch_fav_gather_redo(st, d_idx, d_offs, B, ctx->reg, (uint32_t)ctx->reg_n, apka, gstat, redo));
+  } else {
+    PROF(0, launch_fav_gather(st, d_idx, d_offs, B, ctx->reg, (uint32_t)ctx->reg_n, apka, gstat));
+  }
   HIPCK(hipEventRecord(J.ev_gather, st));
   // The MSM covers every decoded signature of a valid aggregate key, before
   // the subgroup checks: a decodable signature outside G2 stays in S, so the

@@ -16,6 +16,13 @@ hipError_t launch_hash_many(hipStream_t st, const uint8_t* msgs, const uint64_t*
 hipError_t launch_sign_many(hipStream_t st, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, size_t n, uint8_t* out, int* ok);
 hipError_t launch_sk_to_pk_many(hipStream_t st, const uint8_t* sks, size_t n, uint8_t* out, int* ok);
 hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B, const RegKey* reg, uint32_t reg_n, G1P* apk, int* status);
+// the affine gather (bls_gather_aff.hip) for batches of >= 1,024 aggregates: scratch of fav_gather_aff_words(B) u32,
+// redo[B] (1 = recompute with launch_fav_gather_redo, the complete-formula kernel on the flagged aggregates only)
+size_t fav_gather_aff_words(size_t B);
+hipError_t launch_fav_gather_aff(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B,
+                                 const RegKey* reg, uint32_t reg_n, G1P* apk, int* status, uint32_t* scr, int* redo);
+hipError_t launch_fav_gather_redo(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B,
+                                  const RegKey* reg, uint32_t reg_n, G1P* apk, int* status, const int* redo);
 // registry entries from k_key_validate output (+ the host validity mask)
 hipError_t launch_reg_pack(hipStream_t st, const G1A* a, const int* ok, size_t n, RegKey* reg, uint8_t* valid);
 hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok, const G2A* sig, const uint64_t* rsc, int* status, G1A* P2, G2A* Q2);

@@ -232,18 +232,30 @@ __global__ void __launch_bounds__(64) k_sk_to_pk_many(const uint8_t* sks32, size
 // levels: the tree was ~45 % of the wave's time).
 template <int L>
 __global__ void __launch_bounds__(64) k_fav_gather_q(const uint32_t* idx, const uint64_t* offs, size_t B,
-                                                     const RegKey* reg, uint32_t reg_n, G1P* apk, int* status) {
+                                                     const RegKey* reg, uint32_t reg_n, G1P* apk, int* status,
+                                                     const int* only) {
   constexpr int IPW = 64 / L;
   __shared__ G1Q sh[64];
   __shared__ int bad[IPW];
   const int sub = (int)threadIdx.x / L, ln = (int)threadIdx.x % L;
   const size_t b = (size_t)blockIdx.x * IPW + sub;
+  // only (launch_fav_gather_redo): just the flagged aggregates, the others keep what k_fav_gather_aff wrote; a
+  // workgroup with none of them leaves at once (a uniform exit, before any barrier)
+  if (only) {
+    bool any = false;
+    for (int s = 0; s < IPW; ++s) {
+      const size_t bb = (size_t)blockIdx.x * IPW + s;
+      any |= bb < B && only[bb] != 0;
+    }
+    if (!any) return;
+  }
+  const bool mine = b < B && (!only || only[b] != 0);
   if ((int)threadIdx.x < IPW) bad[threadIdx.x] = 0;
   __syncthreads();
   G1Q acc{fq_zero(), fq_unpack(FP_ONE), fq_zero()};  // identity (0 : 1 : 0)
   int mybad = 0;
   uint64_t lo = 0, hi = 0;
-  if (b < B) {
+  if (mine) {
     lo = offs[b];
     hi = offs[b + 1];
     // software pipeline: the record of key j + L and the index of key j + 2L are in flight while key j is added
@@ -288,7 +300,7 @@ __global__ void __launch_bounds__(64) k_fav_gather_q(const uint32_t* idx, const 
     if (ln < s) sh[threadIdx.x] = g1q_add(sh[threadIdx.x], sh[threadIdx.x + s]);
     __syncthreads();
   }
-  if (ln == 0 && b < B) {  // canonical projective aggregate key; the identity is invalid (KeyValidate of the sum)
+  if (ln == 0 && mine) {  // canonical projective aggregate key; the identity is invalid (KeyValidate of the sum)
     const G1Q& a = sh[threadIdx.x];
     const G1P o{fq_pack(a.x), fq_pack(a.y), fq_pack(a.z)};
     apk[b] = o;
@@ -520,9 +532,17 @@ hipError_t launch_fav_gather(hipStream_t st, const uint32_t* idx, const uint64_t
   // a 4-level tree beat 8 + 6 levels of 64 lanes -- C3 +4 %, profiles/r03u_inv_gather_ab.txt), else 64 (a few
   // aggregates spread over more lanes: shorter chains)
   if (B >= 1024)
-    LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status);
+    LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status,
+           (const int*)nullptr);
   else
-    LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status);
+    LAUNCH(k_fav_gather_q<64>, (unsigned)B, 64, st, idx, offs, B, reg, reg_n, apk, status, (const int*)nullptr);
+  return hipSuccess;
+}
+// the aggregates k_fav_gather_aff flagged (redo[b]): complete formulas, the others left as they are
+hipError_t launch_fav_gather_redo(hipStream_t st, const uint32_t* idx, const uint64_t* offs, size_t B,
+                                  const RegKey* reg, uint32_t reg_n, G1P* apk, int* status, const int* redo) {
+  if (!B) return hipSuccess;
+  LAUNCH(k_fav_gather_q<16>, (unsigned)((B + 3) / 4), 64, st, idx, offs, B, reg, reg_n, apk, status, redo);
   return hipSuccess;
 }
 hipError_t launch_av_items(hipStream_t st, size_t B, const uint64_t* io, const int* pk_ok, const int* sig_ok,

@@ -66,7 +66,7 @@ def test_rccl_empty_shard_joins_the_exchange():
     offs = batch.DeviceBuffer(ctx, np.zeros(1, dtype=np.uint64))
     seed = os.urandom(32)
     # no communicator: an empty job is an argument error
-    assert ctx.lib.bls_fav_job_submit_dev(ctx.h, 1, None, offs.ptr, 0, None, None, seed) == -1
+    assert ctx.lib.bls_fav_job_submit_dev(ctx.h, 1, None, offs.ptr, 0, None, None, seed) == -2  # BLS_E_ARG
     dist.init_comm(ctx, 0, 1, DictStore())
     try:
         assert ctx.lib.bls_fav_job_submit_dev(ctx.h, 1, None, offs.ptr, 0, None, None, seed) == 1
