@@ -7,11 +7,14 @@
 //   k_sig_decode      signature decompression + RLC scalar, one lane per item
 //   k_g1_affine_b     r_i apk_i to affine (after k_sig_lane2, bls_chain_lane.hip)
 //   k_h2c_fallback    the reference-path hash_to_G2 for flagged items
+#include <cstdlib>
+#include <cstring>
 #include <utility>
 
 #include "bls_kernels.h"
 #include "bls_lane.h"
 #include "bls_fq_g2.h"
+#include "bls_fq_g2pair.h"
 #include "bls_pp_lane.h"
 #include "bls_vm.h"
 #include "bls_xmd32.h"
@@ -351,6 +354,65 @@ __global__ void __launch_bounds__(64) k_g2x_post1t(size_t B, const int* status, 
 }
 
 
+// The same two kernels on a LANE PAIR per item (bls_fq_g2pair.h: the [|x|] chain in the F2 layout, each lane one
+// coefficient of every Fp2; the complete-formula steps by pp2_add / pp2_dbl, whose products are split between the
+// two lanes).  Every value is the one-lane kernels' (the same expressions per coefficient), so H and the exception
+// flags are identical; the chain's latency halves and a lane holds half the point.  Both lanes write whole staged
+// points (identical values), so every re-read is of the lane's own stores.
+__device__ __forceinline__ PP<Fp2> pp_mul_xabs_pair(const PP<Fp2>& P, bool& exc, uint32_t* lds, bool hi) {
+  const Fq z = q2p_own(P.z, hi);
+  const J2P J{q2p_mul(q2p_own(P.x, hi), z, hi), q2p_mul(q2p_own(P.y, hi), q2p_sqr(z, hi), hi), z};
+  const J2P M = j2p_mul_xabs_lds(J, exc, lds, hi);
+  return PP<Fp2>{q2p_join(q2p_mul(M.x, M.z, hi), hi), q2p_join(M.y, hi),
+                 q2p_join(q2p_mul(q2p_sqr(M.z, hi), M.z, hi), hi)};
+}
+
+__global__ void __launch_bounds__(64) k_g2x_pre2(size_t B, const int* status, Fd* hf, int* flag) {
+  __shared__ uint32_t lds[42 * 64];
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B || (status && !status[i])) return;  // both lanes of an item leave together
+  Fd* r = hf + HCF * i;
+  bool exc = false;
+  // M = [|x|] Q, staged by BOTH lanes (the same values): each lane re-reads its own stores below
+  pp_store1(r + HCF_M, pp_mul_xabs_pair(pp2_load(r + HCF_Q), exc, lds, hi));
+  // the complete-formula steps of k_g2x_pre1t, each from points re-read from the staging slots, products split
+  // over the pair (pp2_add / pp2_dbl)
+  H2C_RELOAD_BARRIER();
+  {
+    const PP<Fp2> pq = pp_psi2x(pp2_load(r + HCF_Q));
+    pp_store1(r + HCF_A, pp2_add(pq, pp_neg2(pp2_load(r + HCF_M)), hi));  // A = psi(Q) - M
+  }
+  H2C_RELOAD_BARRIER();
+  {
+    const PP<Fp2> Q = pp2_load(r + HCF_Q);
+    const PP<Fp2> pq = pp_psi2x(Q);
+    const PP<Fp2> t3{f2mul(Q.x, PSI2_CX), f2mul(Q.y, PSI2_CY), Q.z};  // psi^2(Q); psi^2(2Q) = 2 psi^2(Q)
+    pp_store1(r + HCF_C, pp2_add(pp2_dbl(t3, hi), pp_neg2(pq), hi));    // psi^2(2Q) - psi(Q)
+  }
+  H2C_RELOAD_BARRIER();
+  {
+    const PP<Fp2> mq = pp2_add(pp2_load(r + HCF_M), pp_neg2(pp2_load(r + HCF_Q)), hi);  // M - Q
+    pp_store1(r + HCF_C, pp2_add(pp2_load(r + HCF_C), mq, hi));
+  }
+  if (exc && !hi) flag[i] = 1;
+}
+
+__global__ void __launch_bounds__(64) k_g2x_post2(size_t B, const int* status, Fd* hf, int* flag) {
+  __shared__ uint32_t lds[42 * 64];
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = t >> 1;
+  const bool hi = (t & 1) != 0;
+  if (i >= B || (status && !status[i])) return;
+  Fd* r = hf + HCF * i;
+  bool exc = false;
+  const PP<Fp2> M = pp_mul_xabs_pair(pp2_load(r + HCF_A), exc, lds, hi);
+  H2C_RELOAD_BARRIER();
+  pp_store1(r + HCF_A, pp2_add(pp2_load(r + HCF_C), pp_neg2(M), hi));  // projective H over the dead A slots
+  if (exc && !hi) flag[i] = 1;
+}
+
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 size_t h2c_scratch_fd(size_t B) { return (size_t)HCF * B; }
@@ -362,8 +424,18 @@ static hipError_t launch_h2c_lane2(hipStream_t st, size_t B, const uint8_t* msgs
     hipLaunchKernelGGL(k_h2c_sswu_iso2<true>, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, status, hf, flag);
   else
     hipLaunchKernelGGL(k_h2c_sswu_iso2<false>, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, msgs, offs, status, hf, flag);
-  hipLaunchKernelGGL(k_g2x_pre1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
-  hipLaunchKernelGGL(k_g2x_post1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
+  // the cofactor clearing on a lane pair per item (k_g2x_pre2 / post2: half the chain latency) for batches below
+  // BLS_H2C_PAIR_MAX items (default 4,096: the C3 epoch's 2,048 and C5's 1,024, whose pipelines wait on the hash
+  // branch -- C3 +9 %), on one lane per item above (full batches are bound by total work, which the pair's operand
+  // exchanges raise: C2 -1 %; profiles/r06l_h2c_pair_ab.txt)
+  static const size_t pair_max = getenv("BLS_H2C_PAIR_MAX") ? (size_t)atol(getenv("BLS_H2C_PAIR_MAX")) : 4096;
+  if (B < pair_max) {
+    hipLaunchKernelGGL(k_g2x_pre2, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, status, hf, flag);
+    hipLaunchKernelGGL(k_g2x_post2, dim3(nblk(2 * B, 64)), dim3(64), 0, st, B, status, hf, flag);
+  } else {
+    hipLaunchKernelGGL(k_g2x_pre1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
+    hipLaunchKernelGGL(k_g2x_post1t, dim3(nblk(B, 64)), dim3(64), 0, st, B, status, hf, flag);
+  }
   hipLaunchKernelGGL(k_h2c_affine_b, dim3(nblk(B, 64 * AFF_K2)), dim3(64), 0, st, B, status, hf, H);
   return hipGetLastError();
 }
