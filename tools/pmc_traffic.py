@@ -13,7 +13,7 @@ import os
 import sys
 from collections import defaultdict
 
-SYMBOLS = {"miller": "k_miller_acc4q<2>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
+SYMBOLS = {"miller": "k_miller_acc4q<4>", "miller_lines": "k_miller_lines2", "fav_gather": "k_fav_gather_q<16>"}
 
 
 def main(path, label, sha):
