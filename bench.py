@@ -79,7 +79,7 @@ MILLER_FUSED = os.environ.get("BLS_MILLER_FUSED") == "1"
 MSM_PAIRS = 64  # the MSM's bit-sum pairs (-2^b G1, U_b) join every batch's Miller loops (bls_msm.hip)
 # pairs per f of k_miller_acc4q<G> on batches of >= ACC_SHARED_MIN items (bls_capi.hip fav_prepare: BLS_ACC_G, default
 # 4), one pair per f below
-ACC_G = {"1": 1, "2": 2}.get(os.environ.get("BLS_ACC_G", "4"), 4)
+ACC_G = {"1": 1, "2": 2, "8": 8}.get(os.environ.get("BLS_ACC_G", "4"), 4)
 ACC_SHARED_MIN = int(os.environ.get("BLS_ACC_SHARED_MIN", "4096"))
 
 

@@ -243,14 +243,19 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
   const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
   const Fq2B<1, fqb_detail::MASK> z2{zero, zero};
   F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
-  // the P coordinate each lane scales its line coefficient by: -x_P (h = 0, as K - x_P) or y_P (h = 1), once
-  // (two named values, not an array: the pair loop is not unrolled and an indexed array went to scratch)
-  // (named values, not an array: the pair loop is unrolled but an indexed array went to scratch)
-  const FqC pa = fqb_canon(h ? P[pi[0]].y : P[pi[0]].x), pb = fqb_canon(h ? P[pi[G > 1 ? 1 : 0]].y : P[pi[G > 1 ? 1 : 0]].x);
-  const FqC pc_ = fqb_canon(h ? P[pi[G > 2 ? 2 : 0]].y : P[pi[G > 2 ? 2 : 0]].x);
-  const FqC pd_ = fqb_canon(h ? P[pi[G > 3 ? 3 : 0]].y : P[pi[G > 3 ? 3 : 0]].x);
-  const auto pc0 = sel(h, pa, zero - pa), pc1 = sel(h, pb, zero - pb);
-  const auto pc2 = sel(h, pc_, zero - pc_), pc3 = sel(h, pd_, zero - pd_);
+  // the P coordinate each lane scales its line coefficient by: -x_P (h = 0, as K - x_P) or y_P (h = 1), formed once
+  // and parked in LDS (word-major, this lane's column): held in registers, G of them pushed the kernel past the
+  // register file (G = 4 ran at 256 VGPR + 256 AGPR, the AGPRs a spill space paid in accvgpr moves)
+  using PcT = decltype(sel(h, zero, zero - zero));
+  __shared__ uint32_t pcs[G][14][64];
+  const int lane = (int)threadIdx.x;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const FqC pv = fqb_canon(h ? P[pi[g]].y : P[pi[g]].x);
+    const PcT pcg = sel(h, pv, zero - pv);
+#pragma unroll
+    for (int w = 0; w < 14; ++w) pcs[g][w][lane] = pcg.x.d[w];
+  }
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = relax<VF, DF>(qq_sqr(f, h, q));
@@ -260,8 +265,11 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const LineIn cur = ld_line(Lb[g], ld, h, q);
+        PcT pcg;
+#pragma unroll
+        for (int w = 0; w < 14; ++w) pcg.x.d[w] = pcs[g][w][lane];
         Fq2B<2, fqb_detail::MASK> l2, l3;
-        qq_line_p(cur, g == 0 ? pc0 : (g == 1 ? pc1 : (g == 2 ? pc2 : pc3)), q, l2, l3);
+        qq_line_p(cur, pcg, q, l2, l3);
         const auto fl = relax<VF, DF>(qq_line(f, h, q, cur.l0, l2, l3));
         f = G == 1 ? fl : sel(live[g], fl, f);
         Lb[g] += step;
@@ -406,7 +414,9 @@ hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const 
   if (ld < n) return hipErrorInvalidValue;
   const size_t ngrp = (n + G - 1) / G;
   const dim3 grid((unsigned)((4 * ngrp + 63) / 64));
-  if (G == 4)
+  if (G == 8)
+    hipLaunchKernelGGL(k_miller_acc4q<8>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
+  else if (G == 4)
     hipLaunchKernelGGL(k_miller_acc4q<4>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   else if (G == 2)
     hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
