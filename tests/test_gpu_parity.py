@@ -118,6 +118,21 @@ def test_hash_to_g2(case):
     assert mi355x_bls.hash_to_G2(hb(case["msg"]), case["dst"].encode()) == hb(case["output"])
 
 
+def test_hash_to_g2_rfc9380_vectors():
+    """The device hash_to_G2 (the per-call wide kernel) against RFC 9380 Appendix
+    J.10.1's published points (tests/golden/rfc9380_hash_to_g2.json, QUUX DST): the raw hash bytes pinned to public
+    vectors, not only to the oracle."""
+    from bls_mi355x.backend import mi355x_bls
+
+    g = _load("rfc9380_hash_to_g2.json")
+    dst = g["dst"].encode()
+    for v in g["vectors"]:
+        pt = ((int(v["x"][0], 16), int(v["x"][1], 16)), (int(v["y"][0], 16), int(v["y"][1], 16)))
+        assert mi355x_bls.hash_to_G2(v["msg"].encode(), dst) == O.g2_compress(pt), v["msg"]
+    # (the FAV batch's lane kernels hash 32-byte signing roots under the POP DST; tests/test_gpu_percall.py::
+    # test_h2c_wide_matches_oracle ties them to the wide kernel checked here)
+
+
 def test_deposit_cli_known_answer(B):
     ka = _load("known_answers.json")
     for key in ("deposit_cli", "deposit_cli_flipped"):
