@@ -563,7 +563,11 @@ def launch_ranks(n: int, argv: list[str], dry_run: bool = False) -> int:
               f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')!r}); refusing to run fewer ranks "
               f"than asked", file=sys.stderr, flush=True)
         return 2
+    import signal
+
     procs = {r: subprocess.Popen(cmd, env=e) for r, e in enumerate(envs)}
+    # a SIGTERM to the launcher (a job scheduler's timeout) ends the ranks too, through the finally below
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(128 + signal.SIGTERM))
     rc = 0
     try:
         while procs:
