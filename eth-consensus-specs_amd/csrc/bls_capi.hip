@@ -968,7 +968,8 @@ int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out) {
 
 // The product of n pairings through each Miller-loop form of the batch path, final-exponentiated: out576[576 k ..]
 // for form k = 0 split (k_miller_lines2 + k_miller_acc4q<2>), 1 fused G = 2, 2 fused G = 1, 3 split G = 4, 4 the
-// wave-program kernel (the reference form of bls_multi_pairing), 5 split G = 8.  Points are decoded without subgroup checks;
+// wave-program kernel (the reference form of bls_multi_pairing), 5 split G = 8, 6 split G = 4 lines first
+// (k_miller_acc4l).  Points are decoded without subgroup checks;
 // identity points are skipped pairs.  Returns 1, or 0 if an encoding is invalid.
 int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, uint8_t* out576) {
   API_ENTER(ctx);
@@ -988,7 +989,7 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
   SCR(S_KZ_F, n, f);
   SCR(S_KZ_FT, n / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
-  SCR(S_PT_OUT, 6 * 576, d_out);
+  SCR(S_PT_OUT, 7 * 576, d_out);
   SCR(S_KZ_J, miller_lines_u32(n), L);
   CK(h2d(ctx, d_in, g1s48, 48 * n));
   CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
@@ -999,9 +1000,13 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
   for (size_t i = 0; i < n; i++)
     if (!a[i] || !b[i]) return 0;
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < 7; ++k) {
     size_t nf = n;
-    if (k == 0 || k == 3 || k == 5) {
+    if (k == 6) {
+      LK(launch_miller_lines(st, Q, n, L));
+      LK(launch_miller_acc4l(st, P, Q, nullptr, n, L, miller_lines_ld(n), f));
+      nf = (n + 3) / 4;
+    } else if (k == 0 || k == 3 || k == 5) {
       const int G = k == 0 ? 2 : (k == 3 ? 4 : 8);
       LK(launch_miller_lines(st, Q, n, L));
       LK(launch_miller_acc4(st, P, Q, nullptr, n, L, miller_lines_ld(n), f, G));
@@ -1016,7 +1021,7 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
     LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
     LK(launch_gt_final_exp(st, fo, d_out + 576 * k));
   }
-  CK(d2h(ctx, out576, d_out, 6 * 576));
+  CK(d2h(ctx, out576, d_out, 7 * 576));
   return 1;
 }
 
@@ -1315,8 +1320,15 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
                                                                 : ACC_SHARED_MIN;
   const int mg = B >= shared_min ? (acc_g == 8 || acc_g == 4 || acc_g == 1 ? acc_g : 2) : 1;
   J.fav_mg = mg;
+  // knob BLS_ACC_LL = 1: G = 4 with each step's four lines multiplied together before they meet f
+  // (k_miller_acc4l: 12 Fp2 products per lane per round of four lines instead of 16, but the Karatsuba sums'
+  // normalisations, selects and exchanges leave it 3 % fewer VALU instructions, 13 % waiting, 5.10 ms per launch
+  // against 4.81: profiles/r06u_acc_ll_ab.txt)
+  static const bool acc_ll = getenv("BLS_ACC_LL") && atoi(getenv("BLS_ACC_LL")) != 0;
   if (fused)
     PROF(5, launch_miller_fused(st, rP, H, status, NP, f, mg));
+  else if (mg == 4 && acc_ll)
+    PROF(5, launch_miller_acc4l(st, rP, H, status, NP, mlines, miller_lines_ld(NP), f));
   else
     PROF(5, launch_miller_acc4(st, rP, H, status, NP, mlines, miller_lines_ld(NP), f, mg));
   PROF(6, launch_fp12_prod_vm(st, f, (NP + mg - 1) / mg, ft, fo));

@@ -83,6 +83,10 @@ hipError_t launch_miller_lines(hipStream_t st, const G2A* Q, size_t n, uint32_t*
 // line records' leading dimension (the n of the launch_miller_lines that wrote them)
 hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                               size_t ld, Fp12* f, int G);
+// the same with four pairs per f and each round's four lines multiplied together before they meet f
+// (k_miller_acc4l); writes ceil(n / 4) values
+hipError_t launch_miller_acc4l(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                               size_t ld, Fp12* f);
 // the whole Miller loop of n pairs in one kernel (k_miller_fused: the G2 side and the f accumulation in the same
 // workgroup, line records in LDS); G = 1 or 2 pairs per f; writes ceil(n / G) values (conjugated, x < 0)
 hipError_t launch_miller_fused(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f, int G);

@@ -127,9 +127,9 @@ __device__ __forceinline__ auto qq6mul(const Fq6B<VX, DX>& X, const Fq6B<VY, DY>
 // one Fp12 squaring on the (h, q) lanes, as q_sqr
 template <uint64_t V, uint64_t D>
 __device__ __forceinline__ auto qq_sqr(const Fq6B<V, D>& own, bool h, bool q) {
-  const auto A = bc6<BH0>(own), Bv = bc6<BH1>(own);  // a and b on every lane
-  const auto X = norm(sel(h, A, A + Bv));
-  const auto Y = norm(sel(h, Bv, A + f6v(Bv)));
+  const auto o = dh6(own);  // the other half: b on h = 0, a on h = 1
+  const auto X = norm(sel(h, o, own + o));
+  const auto Y = norm(sel(h, own, own + f6v(o)));
   const auto P = qq6mul(X, Y, q);
   const auto t = bc6<BH1>(P);  // a b (the h = 1 lanes' product)
   return norm(sel(h, P + P, (P - t) - f6v(t)));
@@ -286,6 +286,244 @@ __global__ void __launch_bounds__(64) k_miller_acc4q(const G1A* P, const G2A* Q,
 }
 
 // ---------------------------------------------------------------------------
+// k_miller_acc4l: four pairs per f with the step's lines multiplied together
+// before they meet f (lines first).  A line is L = C + D w with C = (l0, l2, 0)
+// and D = (0, l3, 0); per round of four lines (one per pair) each lane forms
+//   LL = L_a L_b for two of the pairs (q = 0: pairs 0, 1; q = 1: pairs 2, 3):
+//        6 Fp2 products, the Karatsuba set of (l0, l2, l3) x (m0, m2, n3),
+//        three per h lane -- LL = (C0, C1, C2) + (0, D1, D2) w
+//   M = LL_0 LL_1: CC' (h = 0) and (C + D)(C' + D') (h = 1) as Fp6 products
+//        split over q, plus DD' (3 products, one per lane 0..2): 15 products
+//   f M: a M0 (h = 0) and b M1 (h = 1) split over q, then (a + b)(M0 + M1)
+//        over all four lanes: 18 products
+// -- 12 Fp2 products per lane per round against 16 for four f x line
+// products (k_miller_acc4q<4>: 4 per line).  The exchanges are quad DPP moves
+// as in k_miller_acc4q (broadcast from quad lane j: quad_perm [j, j, j, j]).
+namespace {
+
+constexpr int BL0 = 0x00, BL1 = 0x55, BL2 = 0xAA, BL3 = 0xFF;
+
+// one line on this lane: l0, l2 = E ZZ (-x_P), l3 = z3 ZZ y_P; the lane scales its h's coefficient (both
+// components: h = 0 E ZZ by -x_P, h = 1 z3 ZZ by y_P) and takes the other from its h partner.  A pair that is not
+// live is the line 1.
+struct LineF {
+  Fq2B<ML_LV, ML_LD> l0;
+  Fq2B<2, fqb_detail::MASK> l2, l3;
+};
+struct LineRaw {
+  Fq2B<ML_LV, ML_LD> l0, e;
+};
+__device__ __forceinline__ LineRaw ld_line_raw(const uint32_t* Li, size_t n, bool h) {
+  LineRaw r;
+  // the lane's coefficient rows start at a per-lane pointer, so every row offset is uniform (per-lane offsets
+  // were hoisted out of the loop as 28 64-bit registers and spilled)
+  const uint32_t* Le = Li + (size_t)(h ? 56 : 28) * n;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    r.l0.c0.x.d[j] = Li[(size_t)j * n];
+    r.l0.c1.x.d[j] = Li[(size_t)(14 + j) * n];
+    r.e.c0.x.d[j] = Le[(size_t)j * n];
+    r.e.c1.x.d[j] = Le[(size_t)(14 + j) * n];
+  }
+  return r;
+}
+template <class PcT>
+__device__ __forceinline__ LineF line_f(const LineRaw& in, bool h, const PcT& pc, bool live) {
+  const Fq2B<2, fqb_detail::MASK> mine{in.e.c0 * pc, in.e.c1 * pc};
+  SEQ();
+  const auto other = dh2(mine);
+  const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
+  const Fq2B<1, fqb_detail::MASK> one2{one, zero}, zero2{zero, zero};
+  LineF r;
+  r.l0 = relax<ML_LV, ML_LD>(sel(live, in.l0, one2));
+  r.l2 = relax<2, fqb_detail::MASK>(sel(live, sel(h, other, mine), zero2));
+  r.l3 = relax<2, fqb_detail::MASK>(sel(live, sel(h, mine, other), zero2));
+  return r;
+}
+
+// M = LL_0 LL_1 for the round's four lines A, B (this q's two pairs); M0 on the h = 0 lanes, M1 on h = 1
+__device__ __forceinline__ auto ll_m(const LineF& A, const LineF& B, bool h, bool q) {
+  // LL = L_a L_b = (C0, C1, C2) + (0, D1, D2) w on both h lanes of this q:
+  //   C0 = l0 m0 + xi l3 n3, C1 = (l0 + l2)(m0 + m2) - l0 m0 - l2 m2, C2 = l2 m2,
+  //   D1 = (l0 + l3)(m0 + n3) - l0 m0 - l3 n3, D2 = (l2 + l3)(m2 + n3) - l2 m2 - l3 n3
+  // (h = 0 forms the three diagonal products, h = 1 the three sums')
+  const auto p0 = sel(h, norm(A.l0 + A.l2), A.l0) * sel(h, norm(B.l0 + B.l2), B.l0);
+  SEQ();
+  const auto p1 = sel(h, norm(A.l0 + A.l3), A.l2) * sel(h, norm(B.l0 + B.l3), B.l2);
+  SEQ();
+  const auto p2 = sel(h, norm(A.l2 + A.l3), A.l3) * sel(h, norm(B.l2 + B.l3), B.l3);
+  SEQ();
+  const auto t0 = bc2<BH0>(p0), t1 = bc2<BH0>(p1), t2 = bc2<BH0>(p2);  // l0 m0, l2 m2, l3 n3
+  const auto u0 = bc2<BH1>(p0), u1 = bc2<BH1>(p1), u2 = bc2<BH1>(p2);  // the sums' products
+  const auto c0 = norm(t0 + xi(t2));
+  const auto c1 = norm(u0 - (t0 + t1));
+  const auto d1 = norm(u1 - (t0 + t2));
+  const auto d2 = norm(u2 - (t1 + t2));
+  // M = LL_0 LL_1 = CC' + v DD' + ((C + D)(C' + D') - CC' - DD') w  (LL_q on the q lanes, the other by a q
+  // exchange).  DD' = (D1 v + D2 v^2)(D1' v + D2' v^2) = (xi (e2 - e0 - e1), xi e1, e0) with e0 = D1 D1',
+  // e1 = D2 D2', e2 = (D1 + D2)(D1' + D2'): one product on each of lanes 0, 1, 2 (lane 3 repeats lane 2's)
+  const auto od1 = dq2(d1);
+  const auto od2 = dq2(d2);
+  const auto xd1 = sel(q, od1, d1);  // LL_0's
+  const auto xd2 = sel(q, od2, d2);
+  const auto yd1 = sel(q, d1, od1);  // LL_1's
+  const auto yd2 = sel(q, d2, od2);
+  const auto e = sel(h, norm(xd1 + xd2), sel(q, xd2, xd1)) * sel(h, norm(yd1 + yd2), sel(q, yd2, yd1));
+  SEQ();
+  // this q's operand of CC' (h = 0) or (C + D)(C' + D') (h = 1), then the other q's
+  const auto x0 = c0;
+  const auto x1 = sel(h, norm(c1 + d1), c1);
+  const auto x2 = sel(h, norm(t1 + d2), t1);
+  const auto y0 = dq2(x0);
+  const auto y1 = dq2(x1);
+  const auto y2 = dq2(x2);
+  const auto X = fq6b(sel(q, y0, x0), sel(q, y1, x1), sel(q, y2, x2));
+  const auto Y = fq6b(sel(q, x0, y0), sel(q, x1, y1), sel(q, x2, y2));
+  const auto K = qq6mul(X, Y, q);  // CC' on h = 0, (C + D)(C' + D') on h = 1
+  const auto e0 = bc2<BL0>(e);
+  const auto e1 = bc2<BL1>(e);
+  const auto e2 = bc2<BL2>(e);
+  const auto DD = fq6b(xi(norm(e2 - (e0 + e1))), xi(e1), e0);
+  const auto K0 = bc6<BH0>(K);
+  return norm(sel(h, norm(K - norm(K0 + DD)), norm(K0 + f6v(DD))));
+}
+
+// f's half parked in LDS ([word][lane], 84 words) while the lines are multiplied together
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ void park6(uint32_t* lds, const Fq6B<V, D>& f, int lane) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&f);
+#pragma unroll
+  for (int i = 0; i < 84; ++i) lds[i * 64 + lane] = w[i];
+}
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq6B<V, D> unpark6(const uint32_t* lds, int lane) {
+  Fq6B<V, D> f;
+  uint32_t* w = reinterpret_cast<uint32_t*>(&f);
+  __asm__ volatile("" ::: "memory");  // read the LDS copy: no store-to-load forwarding of the parked words
+#pragma unroll
+  for (int i = 0; i < 84; ++i) w[i] = lds[i * 64 + lane];
+  return f;
+}
+
+// f M with f's half (a on h = 0, b on h = 1) read back from LDS:
+//   a' = a M0 + v b M1, b' = (a + b)(M0 + M1) - a M0 - b M1
+// a M0 / b M1 split over q; (a + b)(M0 + M1)'s six products over the four quad lanes in two rounds (lane j =
+// 2h + q: {X0 Y0, X1 Y1, X2 Y2, (X1 + X2)(Y1 + Y2)}[j], then lanes 0 / 1 (2 / 3 as copies) (X0 + X1)(Y0 + Y1),
+// (X0 + X2)(Y0 + Y2))
+template <uint64_t V, uint64_t D, uint64_t VM, uint64_t DM>
+__device__ __forceinline__ auto ll_fm(const uint32_t* fpark, const Fq6B<VM, DM>& M, bool h, bool q, int lane) {
+  auto f = unpark6<V, D>(fpark, lane);
+  const auto Z = qq6mul(f, M, q);  // a M0 on h = 0, b M1 on h = 1
+  SEQ();
+  const auto X = norm(f + dh6(f));  // a + b
+  const auto xa = sel(h, sel(q, norm(X.c1 + X.c2), X.c2), sel(q, X.c1, X.c0));
+  const auto xb = sel(q, norm(X.c0 + X.c2), norm(X.c0 + X.c1));
+  const auto Y = norm(M + dh6(M));  // M0 + M1
+  const auto ya = sel(h, sel(q, norm(Y.c1 + Y.c2), Y.c2), sel(q, Y.c1, Y.c0));
+  const auto yb = sel(q, norm(Y.c0 + Y.c2), norm(Y.c0 + Y.c1));
+  const auto pa = xa * ya;
+  SEQ();
+  const auto pb = xb * yb;
+  SEQ();
+  const auto r0 = bc2<BL0>(pa), r1 = bc2<BL1>(pa), r2 = bc2<BL2>(pa), r3 = bc2<BL3>(pa);
+  const auto s0 = bc2<BL0>(pb), s1 = bc2<BL1>(pb);
+  const auto S = fq6b(norm(xi(norm(r3 - (r1 + r2))) + r0), norm((s0 - (r0 + r1)) + xi(r2)),
+                      norm((s1 - (r0 + r2)) + r1));
+  const auto Zo = dh6(Z);
+  return norm(sel(h, S - norm(Z + Zo), Z + f6v(Zo)));
+}
+
+}  // namespace
+
+// four pairs per f, lines first; the records and the output as k_miller_acc4q<4>
+__global__ void __launch_bounds__(64) k_miller_acc4l(const G1A* P, const G2A* Q, const int* ok, size_t n,
+                                                     const uint32_t* L, size_t ld, Fp12* out) {
+  constexpr int G = 4;
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t grp = t >> 2;
+  const bool h = (t & 2) != 0, q = (t & 1) != 0;
+  const size_t ngrp = (n + G - 1) / G;
+  if (grp >= ngrp) return;  // the four lanes of a group leave together
+  bool any = false, live[2];
+  size_t pi[2];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const size_t p = grp * G + g;
+    const size_t pc = p < n ? p : n - 1;  // clamped: loads stay inside the batch's line buffer
+    const bool lv = p < n && (!ok || ok[p]) && !P[p].inf && !Q[p].inf;
+    any = any || lv;
+    if ((g >> 1) == (int)q) {  // this lane's pairs: 2q, 2q + 1
+      live[g & 1] = lv;
+      pi[g & 1] = pc;
+    }
+  }
+  if (!any) {
+    if (!q) {
+      Fp6* o = h ? &out[grp].c1 : &out[grp].c0;
+      *o = h ? Fp6{fp2_zero(), fp2_zero(), fp2_zero()} : Fp6{fp2_one(), fp2_zero(), fp2_zero()};
+    }
+    return;
+  }
+  constexpr uint64_t VF = ML_QF_V, DF = ML_QF_D;
+  using F = Fq6B<VF, DF>;
+  const size_t step = (size_t)ML_WORDS * ld;
+  const uint32_t* La = L + pi[0];
+  const uint32_t* Lb = L + pi[1];
+  const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
+  const Fq2B<1, fqb_detail::MASK> z2{zero, zero};
+  F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
+  // this lane's P coordinate of each of its two pairs (-x_P as K - x_P on h = 0, y_P on h = 1), parked in LDS
+  using PcT = decltype(sel(h, zero, zero - zero));
+  __shared__ uint32_t pcs[2][14][64];
+  __shared__ uint32_t fpark[84 * 64];
+  const int lane = (int)threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const FqC pv = fqb_canon(h ? P[pi[s]].y : P[pi[s]].x);
+    const PcT pcg = sel(h, pv, zero - pv);
+#pragma unroll
+    for (int w = 0; w < 14; ++w) pcs[s][w][lane] = pcg.x.d[w];
+  }
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = relax<VF, DF>(qq_sqr(f, h, q));
+    const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
+#pragma unroll 1
+    for (int s = 0; s < nl; ++s) {
+      // opaque line pointers: otherwise loop strength reduction keeps one 64-bit induction pointer per record
+      // row (56 per pair) across the loop, and they spill
+      __asm__ volatile("" : "+v"(La), "+v"(Lb));
+      const LineRaw ra = ld_line_raw(La, ld, h);  // both pairs' loads in flight while f is parked
+      const LineRaw rb = ld_line_raw(Lb, ld, h);
+      park6(fpark, f, lane);
+      SEQ();
+      PcT pa, pb;
+#pragma unroll
+      for (int w = 0; w < 14; ++w) pa.x.d[w] = pcs[0][w][lane];
+      const LineF A = line_f(ra, h, pa, live[0]);
+      SEQ();
+#pragma unroll
+      for (int w = 0; w < 14; ++w) pb.x.d[w] = pcs[1][w][lane];
+      const LineF B = line_f(rb, h, pb, live[1]);
+      SEQ();
+      const auto M = ll_m(A, B, h, q);
+      SEQ();
+      f = relax<VF, DF>(ll_fm<VF, DF>(fpark, M, h, q, lane));
+      SEQ();
+      La += step;
+      Lb += step;
+    }
+  }
+  if (!q) {
+    Fp6 r{fq2b_pack(f.c0), fq2b_pack(f.c1), fq2b_pack(f.c2)};
+    if (h)
+      out[grp].c1 = Fp6{fp2_neg(r.c0), fp2_neg(r.c1), fp2_neg(r.c2)};
+    else
+      out[grp].c0 = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_miller_fused<G>: both halves of the split Miller loop in ONE workgroup per MF_PAIRS<G> pairs.  Wave 0 runs
 // the G2 side and writes each line record into an LDS double buffer; waves 1 and 2 run the f accumulation (four
 // lanes per f, G pairs per f, the code of k_miller_acc4q) and read the record of line k while wave 0 forms line k
@@ -422,6 +660,15 @@ hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const 
     hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   else
     hipLaunchKernelGGL(k_miller_acc4q<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_miller_acc4l(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                               size_t ld, Fp12* f) {
+  if (!n) return hipSuccess;
+  if (ld < n) return hipErrorInvalidValue;
+  const size_t ngrp = (n + 3) / 4;
+  hipLaunchKernelGGL(k_miller_acc4l, dim3((unsigned)((4 * ngrp + 63) / 64)), dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   return hipGetLastError();
 }
 

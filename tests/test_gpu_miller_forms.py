@@ -1,5 +1,6 @@
 """GPU parity of the Miller-loop forms of the batch path (bls_test_miller_forms): the split kernels (the G2 lines of
-k_miller_lines2 + the f accumulation of k_miller_acc4q, two, four or eight pairs per f), the fused kernel
+k_miller_lines2 + the f accumulation of k_miller_acc4q, two, four or eight pairs per f, and k_miller_acc4l: four
+pairs per f with each step's lines multiplied together before they meet f), the fused kernel
 (k_miller_fused: lines formed in LDS by a line wave, one or two pairs per f) and the wave-program kernel of
 bls_multi_pairing -- the final exponentiation of each form's product must be the same GT element, and equal the
 oracle's pairing product (oracle/bls_oracle.py).  Pair counts are chosen off every multiple the kernels group by
@@ -13,7 +14,7 @@ from oracle import bls_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-FORMS = ("split G=2", "fused G=2", "fused G=1", "split G=4", "wave program", "split G=8")
+FORMS = ("split G=2", "fused G=2", "fused G=1", "split G=4", "wave program", "split G=8", "split G=4 lines first")
 
 
 def _gt_bytes(f):
@@ -38,16 +39,16 @@ def _forms(ps, qs):
     ctx = _native.context()
     g1 = b"".join(O.g1_compress(p) for p in ps)
     g2 = b"".join(O.g2_compress(q) for q in qs)
-    out = ctypes.create_string_buffer(6 * 576)
+    out = ctypes.create_string_buffer(len(FORMS) * 576)
     assert ctx.check(ctx.lib.bls_test_miller_forms(ctx.h, g1, g2, len(ps), out)) == 1
-    return [out.raw[576 * k: 576 * k + 576] for k in range(6)]
+    return [out.raw[576 * k: 576 * k + 576] for k in range(len(FORMS))]
 
 
-@pytest.mark.parametrize("n,ids", [(5, (2,)), (37, (0, 36)), (131, (64, 65, 130))])
+@pytest.mark.parametrize("n,ids", [(5, (2,)), (37, (0, 36)), (131, (64, 65, 130)), (13, (4, 5, 6, 7, 9, 10))])
 def test_miller_forms_agree_with_the_oracle(n, ids):
     ps, qs = _pairs(n, 1000 + n, ids)
     got = _forms(ps, qs)
-    for k in range(1, 6):
+    for k in range(1, len(FORMS)):
         assert got[k] == got[0], FORMS[k]
     if n <= 5:  # the oracle's pairing product (slow in Python: small n only)
         f = O.F12_ONE
@@ -61,4 +62,4 @@ def test_miller_forms_full_workgroups():
     """700 pairs: eleven fused G=2 workgroups (the last one short), 22 G=1 workgroups, partial waves of f."""
     ps, qs = _pairs(700, 77, identities=(0, 1, 63, 64, 699))
     got = _forms(ps, qs)
-    assert all(g == got[0] for g in got), [FORMS[k] for k in range(6) if got[k] != got[0]]
+    assert all(g == got[0] for g in got), [FORMS[k] for k in range(len(FORMS)) if got[k] != got[0]]
