@@ -109,6 +109,89 @@ __global__ void __launch_bounds__(64) k_fe_check_gated(const Fp12* node, const i
   fe_check_body(s, &bad, node + b, 1, res + b);
 }
 
+// Products of consecutive chunks, out[b] = prod in[b chunk .. min(n, (b + 1) chunk)), with the lane-parallel
+// Fp12 product of the final exponentiation (three phases over the 64 lanes; the wave-program product of
+// k_fp12_chunk_prod runs each step on a few lanes)
+__global__ void __launch_bounds__(64) k_fp12_chunk_prod_fe(const Fp12* in, size_t n, int chunk, Fp12* outp) {
+  __shared__ FeSlot s[FE_NSLOT];
+  const int lane = threadIdx.x;
+  const size_t lo = (size_t)blockIdx.x * chunk;
+  const size_t hi = lo + chunk < n ? lo + chunk : n;
+  fe_load_consts(s, lane, 64);
+  FeDev ex;
+  ex.s = s;
+  ex.lane = lane;
+  ex.init();
+  for (size_t i = lo; i < hi; i++) {
+    if (lane < 12) fe_st(s, 12 * (i != lo ? 1 : 0) + lane, fq_unpack(reinterpret_cast<const Fp*>(in + i)[lane]));
+    __syncthreads();
+    if (i != lo) ex.mul(0, 1, 0);
+  }
+  if (lane < 12) reinterpret_cast<Fp*>(outp + blockIdx.x)[lane] = fq_pack(fe_ld(s, lane));
+}
+
+// out[b] = prod_{i in chunk b} a[i] b[i] (the bisection tree's leaves), as k_fp12_chunk_prod2
+__global__ void __launch_bounds__(64) k_fp12_chunk_prod2_fe(const Fp12* a, const Fp12* b, size_t n, int chunk,
+                                                             Fp12* outp) {
+  __shared__ FeSlot s[FE_NSLOT];
+  const int lane = threadIdx.x;
+  const size_t lo = (size_t)blockIdx.x * chunk;
+  const size_t hi = lo + chunk < n ? lo + chunk : n;
+  fe_load_consts(s, lane, 64);
+  FeDev ex;
+  ex.s = s;
+  ex.lane = lane;
+  ex.init();
+  for (size_t i = lo; i < hi; i++) {
+    if (lane < 12) fe_st(s, 12 * (i != lo ? 1 : 0) + lane, fq_unpack(reinterpret_cast<const Fp*>(a + i)[lane]));
+    __syncthreads();
+    if (i != lo) ex.mul(0, 1, 0);
+    if (lane < 12) fe_st(s, 12 + lane, fq_unpack(reinterpret_cast<const Fp*>(b + i)[lane]));
+    __syncthreads();
+    ex.mul(0, 1, 0);
+  }
+  if (lane < 12) reinterpret_cast<Fp*>(outp + blockIdx.x)[lane] = fq_pack(fe_ld(s, lane));
+}
+
+// ragged segments out[b] = prod in[io[b] + b .. io[b + 1] + b] (inclusive), as k_fp12_seg_prod
+__global__ void __launch_bounds__(64) k_fp12_seg_prod_fe(const Fp12* in, const uint64_t* io, Fp12* outp) {
+  __shared__ FeSlot s[FE_NSLOT];
+  const int lane = threadIdx.x;
+  const size_t b = blockIdx.x;
+  const size_t lo = io[b] + b, hi = io[b + 1] + b + 1;
+  fe_load_consts(s, lane, 64);
+  FeDev ex;
+  ex.s = s;
+  ex.lane = lane;
+  ex.init();
+  for (size_t i = lo; i < hi; i++) {
+    if (lane < 12) fe_st(s, 12 * (i != lo ? 1 : 0) + lane, fq_unpack(reinterpret_cast<const Fp*>(in + i)[lane]));
+    __syncthreads();
+    if (i != lo) ex.mul(0, 1, 0);
+  }
+  if (lane < 12) reinterpret_cast<Fp*>(outp + b)[lane] = fq_pack(fe_ld(s, lane));
+}
+
+hipError_t launch_fp12_chunk_prod2_fe(hipStream_t st, const Fp12* a, const Fp12* b, size_t n, int chunk, Fp12* out) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_chunk_prod2_fe, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, a, b, n, chunk,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fp12_seg_prod_fe(hipStream_t st, const Fp12* in, const uint64_t* io, size_t B, Fp12* out) {
+  if (!B) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_seg_prod_fe, dim3((unsigned)B), dim3(64), 0, st, in, io, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fp12_chunk_prod_fe(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fp12_chunk_prod_fe, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, in, n, chunk,
+                     out);
+  return hipGetLastError();
+}
+
 hipError_t launch_final_check_wave(hipStream_t st, const Fp12* f, int n, int* out) {
   hipLaunchKernelGGL(k_fe_check, dim3(1), dim3(64), 0, st, f, n, (const uint32_t*)nullptr, out);
   return hipGetLastError();

@@ -113,6 +113,10 @@ hipError_t launch_g1_affine(hipStream_t st, size_t B, const int* status, const G
 hipError_t launch_final_check_sel(hipStream_t st, const Fp12* f, const uint32_t* sel, size_t nsel, int* out);
 hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out);
 hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* tmp, Fp12* out);
+// out[b] = prod in[b chunk .. (b + 1) chunk) with the final exponentiation's lane-parallel product (bls_fe.hip)
+hipError_t launch_fp12_chunk_prod_fe(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out);
+hipError_t launch_fp12_chunk_prod2_fe(hipStream_t st, const Fp12* a, const Fp12* b, size_t n, int chunk, Fp12* out);
+hipError_t launch_fp12_seg_prod_fe(hipStream_t st, const Fp12* in, const uint64_t* io, size_t B, Fp12* out);
 
 // curve objects (bls_points.hip): group 1 = G1 (48-B encodings, G1A), 2 = G2 (96-B, G2A)
 hipError_t launch_pt_decode(hipStream_t st, int group, const uint8_t* in, size_t n, int subgroup, void* out, int* ok);

@@ -133,7 +133,16 @@ __global__ void __launch_bounds__(64) k_fp12_seg_prod(const Fp12* in, const uint
   if (threadIdx.x < 12) fp12_slot_dst(outp[b], threadIdx.x) = fp_from_fd(s[base + threadIdx.x]);
 }
 
+// Every Fp12 product tree runs on the final exponentiation's lane-parallel product (bls_fe.hip *_fe kernels: three
+// phases over the 64 lanes per product, where the wave program keeps most lanes idle): C3 +2.8 %
+// (profiles/r06v_prod_fe_ab.txt).  Knob BLS_PROD_VM = 1: the wave-program kernels of this file.
+static bool prod_fe() {
+  static const bool on = !(getenv("BLS_PROD_VM") && atoi(getenv("BLS_PROD_VM")) != 0);
+  return on;
+}
+
 hipError_t launch_fp12_seg_prod(hipStream_t st, const Fp12* in, const uint64_t* io, size_t B, Fp12* out) {
+  if (prod_fe()) return launch_fp12_seg_prod_fe(st, in, io, B, out);
   if (!B) return hipSuccess;
   hipLaunchKernelGGL(k_fp12_seg_prod, dim3((unsigned)B), dim3(64), 0, st, in, io, B, out);
   return hipGetLastError();
@@ -146,12 +155,14 @@ hipError_t launch_miller_wave(hipStream_t st, const G1A* P, const G2A* Q, const 
 }
 
 hipError_t launch_fp12_chunk_prod(hipStream_t st, const Fp12* in, size_t n, int chunk, Fp12* out) {
+  if (prod_fe()) return launch_fp12_chunk_prod_fe(st, in, n, chunk, out);
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_fp12_chunk_prod, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, in, n, chunk, out);
   return hipGetLastError();
 }
 
 hipError_t launch_fp12_chunk_prod2(hipStream_t st, const Fp12* a, const Fp12* b, size_t n, int chunk, Fp12* out) {
+  if (prod_fe()) return launch_fp12_chunk_prod2_fe(st, a, b, n, chunk, out);
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_fp12_chunk_prod2, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(64), 0, st, a, b, n, chunk,
                      out);
@@ -167,8 +178,7 @@ hipError_t launch_fp12_prod_vm(hipStream_t st, const Fp12* in, size_t n, Fp12* t
     const int chunk = n > 64 ? 16 : (int)n;
     const size_t blocks = (n + chunk - 1) / chunk;
     Fp12* dst = blocks == 1 ? out : bufs[w];
-    hipLaunchKernelGGL(k_fp12_chunk_prod, dim3((unsigned)blocks), dim3(64), 0, st, cur, n, chunk, dst);
-    hipError_t e = hipGetLastError();
+    const hipError_t e = launch_fp12_chunk_prod(st, cur, n, chunk, dst);
     if (e != hipSuccess) return e;
     cur = dst;
     n = blocks;
