@@ -969,7 +969,7 @@ int bls_test_h2c_wide_stages(bls_ctx* ctx, const uint8_t* msg32, uint8_t* out) {
 // The product of n pairings through each Miller-loop form of the batch path, final-exponentiated: out576[576 k ..]
 // for form k = 0 split (k_miller_lines2 + k_miller_acc4q<2>), 1 fused G = 2, 2 fused G = 1, 3 split G = 4, 4 the
 // wave-program kernel (the reference form of bls_multi_pairing), 5 split G = 8, 6 split G = 4 lines first
-// (k_miller_acc4l).  Points are decoded without subgroup checks;
+// (k_miller_acc4l), 7 split G = 1 on eight lanes per f (k_miller_acc8).  Points are decoded without subgroup checks;
 // identity points are skipped pairs.  Returns 1, or 0 if an encoding is invalid.
 int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, uint8_t* out576) {
   API_ENTER(ctx);
@@ -989,7 +989,7 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
   SCR(S_KZ_F, n, f);
   SCR(S_KZ_FT, n / 8 + 16, ft);
   SCR(S_FPART, 1, fo);
-  SCR(S_PT_OUT, 7 * 576, d_out);
+  SCR(S_PT_OUT, 8 * 576, d_out);
   SCR(S_KZ_J, miller_lines_u32(n), L);
   CK(h2d(ctx, d_in, g1s48, 48 * n));
   CK(h2d(ctx, d_in + 48 * n, g2s96, 96 * n));
@@ -1000,9 +1000,12 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
   CK(d2h(ctx, b.data(), ok2, n * sizeof(int)));
   for (size_t i = 0; i < n; i++)
     if (!a[i] || !b[i]) return 0;
-  for (int k = 0; k < 7; ++k) {
+  for (int k = 0; k < 8; ++k) {
     size_t nf = n;
-    if (k == 6) {
+    if (k == 7) {
+      LK(launch_miller_lines(st, Q, n, L));
+      LK(launch_miller_acc8(st, P, Q, nullptr, n, L, miller_lines_ld(n), f));
+    } else if (k == 6) {
       LK(launch_miller_lines(st, Q, n, L));
       LK(launch_miller_acc4l(st, P, Q, nullptr, n, L, miller_lines_ld(n), f));
       nf = (n + 3) / 4;
@@ -1021,7 +1024,7 @@ int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s
     LK(launch_fp12_prod_vm(st, f, nf, ft, fo));
     LK(launch_gt_final_exp(st, fo, d_out + 576 * k));
   }
-  CK(d2h(ctx, out576, d_out, 7 * 576));
+  CK(d2h(ctx, out576, d_out, 8 * 576));
   return 1;
 }
 
@@ -1186,6 +1189,7 @@ static bool miller_fused() {
   static const bool on = getenv("BLS_MILLER_FUSED") && !strcmp(getenv("BLS_MILLER_FUSED"), "1");
   return on;
 }
+constexpr size_t ACC8_MAX = 2048;  // items per FAV batch below which one pair per f runs on eight lanes
 constexpr size_t ACC_SHARED_MIN = 4096;  // items per FAV batch from which k_miller_acc4q shares f between two pairs
 
 static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_offs, size_t B, const uint8_t* d_msgs,
@@ -1325,8 +1329,14 @@ static int fav_prepare(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_of
   // normalisations, selects and exchanges leave it 3 % fewer VALU instructions, 13 % waiting, 5.10 ms per launch
   // against 4.81: profiles/r06u_acc_ll_ab.txt)
   static const bool acc_ll = getenv("BLS_ACC_LL") && atoi(getenv("BLS_ACC_LL")) != 0;
+  // below ACC8_MAX items one pair per f runs on eight lanes (k_miller_acc8: ~40 % fewer product rounds per step for
+  // twice the waves): a latency win for the small batches whose chain decides (C5's 1,024: +2.4 %), a loss where
+  // the SIMD time does (C3's 2,048: -8.6 %; profiles/r06y_acc8_ab.txt).  Knob BLS_ACC8_MAX.
+  static const size_t acc8_max = getenv("BLS_ACC8_MAX") ? (size_t)atol(getenv("BLS_ACC8_MAX")) : ACC8_MAX;
   if (fused)
     PROF(5, launch_miller_fused(st, rP, H, status, NP, f, mg));
+  else if (mg == 1 && B < acc8_max)
+    PROF(5, launch_miller_acc8(st, rP, H, status, NP, mlines, miller_lines_ld(NP), f));
   else if (mg == 4 && acc_ll)
     PROF(5, launch_miller_acc4l(st, rP, H, status, NP, mlines, miller_lines_ld(NP), f));
   else
@@ -2076,7 +2086,13 @@ static int job_submit(bls_ctx* ctx, const uint32_t* d_idx, const uint64_t* d_off
   // bls_fav_job_check_own (no host round trip of the partial), and a multi-GPU failure is localised by it
   int* d_own;
   SCR(S_OWN, 1, d_own);
-  PROF(7, launch_final_check_wave(J.stream, f, 1, d_own));
+  // knob BLS_FE_WIDE_MAX: the check of batches below that size on the six-wave k_fe_wide (0.65 ms against 1.13, six
+  // waves against one): C3 -4.5 %, C5 unchanged (profiles/r06y_acc8_ab.txt), so off
+  static const size_t fe_wide_max = getenv("BLS_FE_WIDE_MAX") ? (size_t)atol(getenv("BLS_FE_WIDE_MAX")) : 0;
+  if (B < fe_wide_max)
+    PROF(7, launch_fe_wide(J.stream, f, 1, d_own));
+  else
+    PROF(7, launch_final_check_wave(J.stream, f, 1, d_own));
   HIPCK(hipMemcpyAsync(J.h_own, d_own, sizeof(int), hipMemcpyDeviceToHost, J.stream));
   HIPCK(hipEventRecord(J.ev_own, J.stream));
   J.own_pending = true;

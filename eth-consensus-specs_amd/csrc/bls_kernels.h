@@ -87,6 +87,9 @@ hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const 
 // (k_miller_acc4l); writes ceil(n / 4) values
 hipError_t launch_miller_acc4l(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
                                size_t ld, Fp12* f);
+// one pair per f on eight lanes (k_miller_acc8, the latency form for small batches); writes n values
+hipError_t launch_miller_acc8(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                              size_t ld, Fp12* f);
 // the whole Miller loop of n pairs in one kernel (k_miller_fused: the G2 side and the f accumulation in the same
 // workgroup, line records in LDS); G = 1 or 2 pairs per f; writes ceil(n / G) values (conjugated, x < 0)
 hipError_t launch_miller_fused(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, Fp12* f, int G);

@@ -524,6 +524,138 @@ __global__ void __launch_bounds__(64) k_miller_acc4l(const G1A* P, const G2A* Q,
 }
 
 // ---------------------------------------------------------------------------
+// k_miller_acc8: one pair per f on EIGHT lanes -- the latency form for small
+// batches.  Lane 8k + 4h + j: h selects the half of f (a = f.c0 / b = f.c1) and
+// the quad of lanes that owns it; j (0..3) which products of each step the lane
+// forms:
+//   squaring   each half's Fp6 product ((a + b)(a + v b) / a b) with its six
+//              Fp2 products over the quad in two rounds (q4_6mul): 2 products
+//              per lane instead of 3
+//   line       the eight Fp2 products of the half's line product two per lane
+//              (k_miller_acc4q<1>: four)
+// The other half of a quad-uniform value comes from the mirrored lane of the
+// other quad (DPP row_half_mirror: lane 4h + j <- lane 4(1 - h) + 3 - j, which
+// holds the same value as every lane of its quad), a product of the quad from
+// one quad broadcast.  Twice the waves of k_miller_acc4q<1> for ~40 % fewer
+// product rounds per step.
+namespace {
+
+__device__ __forceinline__ uint32_t dpp_m(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+}
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ FqB<V, D> dm(const FqB<V, D>& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = dpp_m(a.x.d[i]);
+  return {r};
+}
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq2B<V, D> dm2(const Fq2B<V, D>& a) {
+  return {dm(a.c0), dm(a.c1)};
+}
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ Fq6B<V, D> dm6(const Fq6B<V, D>& a) {
+  return {dm2(a.c0), dm2(a.c1), dm2(a.c2)};
+}
+
+// the Fp6 product X Y with its six Fp2 products over the four quad lanes in two rounds (lane j = 2 j1 + j0 forms
+// {X0 Y0, X1 Y1, X2 Y2, (X1 + X2)(Y1 + Y2)}[j], then lanes 0 / 1 (and, as copies, 2 / 3) (X0 + X1)(Y0 + Y1) /
+// (X0 + X2)(Y0 + Y2)); X and Y are the same on every lane of the quad, and so is the result
+template <uint64_t VX, uint64_t DX, uint64_t VY, uint64_t DY>
+__device__ __forceinline__ auto q4_6mul(const Fq6B<VX, DX>& X, const Fq6B<VY, DY>& Y, bool j1, bool j0) {
+  const auto p1 = sel(j1, sel(j0, norm(X.c1 + X.c2), X.c2), sel(j0, X.c1, X.c0)) *
+                  sel(j1, sel(j0, norm(Y.c1 + Y.c2), Y.c2), sel(j0, Y.c1, Y.c0));
+  SEQ();
+  const auto p2 = sel(j0, norm(X.c0 + X.c2), norm(X.c0 + X.c1)) * sel(j0, norm(Y.c0 + Y.c2), norm(Y.c0 + Y.c1));
+  SEQ();
+  const auto r0 = bc2<BL0>(p1), r1 = bc2<BL1>(p1), r2 = bc2<BL2>(p1), r3 = bc2<BL3>(p1);
+  const auto s0 = bc2<BL0>(p2), s1 = bc2<BL1>(p2);
+  const auto c0 = norm(xi(norm(r3 - (r1 + r2))) + r0);
+  const auto c1 = norm((s0 - (r0 + r1)) + xi(r2));
+  const auto c2 = norm((s1 - (r0 + r2)) + r1);
+  return fq6b(c0, c1, c2);
+}
+
+// one Fp12 squaring on the eight lanes (j1 j0 = j)
+template <uint64_t V, uint64_t D>
+__device__ __forceinline__ auto q8_sqr(const Fq6B<V, D>& own, bool h, bool j1, bool j0) {
+  const auto o = dm6(own);  // the other half
+  const auto X = norm(sel(h, o, own + o));
+  const auto Y = norm(sel(h, own, own + f6v(o)));
+  const auto P = q4_6mul(X, Y, j1, j0);  // (a + b)(a + v b) on h = 0, a b on h = 1
+  const auto t = dm6(P);                 // a b on the h = 0 lanes
+  return norm(sel(h, P + P, (P - t) - f6v(t)));
+}
+
+// own *= line (l0 + l2 v) + l3 v w, the eight products of qq_line two per lane:
+//   round 1: a0 l0, a1 l2, a2 l2, a2 l0;  round 2: (a0 + a1)(l0 + l2), o2 l3, o0 l3, o1 l3  (lane j: the j-th)
+template <uint64_t V, uint64_t D, uint64_t VL, uint64_t DL, uint64_t VM, uint64_t DM>
+__device__ __forceinline__ auto q8_line(const Fq6B<V, D>& own, bool h, bool j1, bool j0, const Fq2B<VL, DL>& l0,
+                                        const Fq2B<VM, DM>& l2, const Fq2B<VM, DM>& l3) {
+  const auto pa = sel(j1, own.c2, sel(j0, own.c1, own.c0)) * sel(j1, sel(j0, l0, l2), sel(j0, l2, l0));
+  SEQ();
+  const auto o = dm6(own);
+  const auto pb = sel(j1, sel(j0, o.c1, o.c0), sel(j0, o.c2, norm(own.c0 + own.c1))) *
+                  sel(j1, l3, sel(j0, l3, norm(l0 + l2)));
+  SEQ();
+  const auto t0 = bc2<BL0>(pa), t1 = bc2<BL1>(pa), u0 = bc2<BL2>(pa), u2 = bc2<BL3>(pa);
+  const auto u1 = bc2<BL0>(pb), v0 = bc2<BL1>(pb), v1 = bc2<BL2>(pb), v2 = bc2<BL3>(pb);
+  const auto m01 = fq6b(t0 + xi(u0), (u1 - (t0 + t1)), t1 + u2);
+  const auto m1 = fq6b(xi(v0), v1, v2);
+  return norm(norm(m01) + sel(h, m1, f6v(m1)));
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_miller_acc8(const G1A* P, const G2A* Q, const int* ok, size_t n,
+                                                    const uint32_t* L, size_t ld, Fp12* out) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t pi = t >> 3;
+  const bool h = (t & 4) != 0, j1 = (t & 2) != 0, j0 = (t & 1) != 0;
+  if (pi >= n) return;  // the eight lanes of a pair leave together
+  const bool live = (!ok || ok[pi]) && !P[pi].inf && !Q[pi].inf;
+  if (!live) {
+    if (!j1 && !j0) {
+      Fp6* o = h ? &out[pi].c1 : &out[pi].c0;
+      *o = h ? Fp6{fp2_zero(), fp2_zero(), fp2_zero()} : Fp6{fp2_one(), fp2_zero(), fp2_zero()};
+    }
+    return;
+  }
+  constexpr uint64_t VF = ML_QF_V, DF = ML_QF_D;
+  using F = Fq6B<VF, DF>;
+  const size_t step = (size_t)ML_WORDS * ld;
+  const uint32_t* Lp = L + pi;
+  const FqC one = fqb_canon(FP_ONE), zero{fq_zero()};
+  const Fq2B<1, fqb_detail::MASK> z2{zero, zero};
+  F f = relax<VF, DF>(Fq6B<1, fqb_detail::MASK>{{sel(h, zero, one), zero}, z2, z2});
+  const FqC pv = fqb_canon(h ? P[pi].y : P[pi].x);
+  const auto pc = sel(h, pv, zero - pv);  // -x_P (h = 0) or y_P (h = 1)
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = relax<VF, DF>(q8_sqr(f, h, j1, j0));
+    const int nl = ((X_ABS >> b) & 1ull) ? 2 : 1;
+#pragma unroll 1
+    for (int s = 0; s < nl; ++s) {
+      const LineIn cur = ld_line(Lp, ld, h, j0);  // l0 and component j0 of this h's coefficient
+      const FqN mine = cur.c * pc;
+      const Fq2B<2, fqb_detail::MASK> m{bc<BL0>(mine), bc<BL1>(mine)};  // this h's coefficient times its P factor
+      const auto mo = dm2(m);
+      const auto l2 = sel(h, mo, m), l3 = sel(h, m, mo);
+      f = relax<VF, DF>(q8_line(f, h, j1, j0, cur.l0, l2, l3));
+      Lp += step;
+    }
+  }
+  if (!j1 && !j0) {
+    Fp6 r{fq2b_pack(f.c0), fq2b_pack(f.c1), fq2b_pack(f.c2)};
+    if (h)
+      out[pi].c1 = Fp6{fp2_neg(r.c0), fp2_neg(r.c1), fp2_neg(r.c2)};
+    else
+      out[pi].c0 = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_miller_fused<G>: both halves of the split Miller loop in ONE workgroup per MF_PAIRS<G> pairs.  Wave 0 runs
 // the G2 side and writes each line record into an LDS double buffer; waves 1 and 2 run the f accumulation (four
 // lanes per f, G pairs per f, the code of k_miller_acc4q) and read the record of line k while wave 0 forms line k
@@ -660,6 +792,14 @@ hipError_t launch_miller_acc4(hipStream_t st, const G1A* P, const G2A* Q, const 
     hipLaunchKernelGGL(k_miller_acc4q<2>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   else
     hipLaunchKernelGGL(k_miller_acc4q<1>, grid, dim3(64), 0, st, P, Q, ok, n, L, ld, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_miller_acc8(hipStream_t st, const G1A* P, const G2A* Q, const int* ok, size_t n, const uint32_t* L,
+                              size_t ld, Fp12* f) {
+  if (!n) return hipSuccess;
+  if (ld < n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_miller_acc8, dim3((unsigned)((8 * n + 63) / 64)), dim3(64), 0, st, P, Q, ok, n, L, ld, f);
   return hipGetLastError();
 }
 

@@ -308,9 +308,9 @@ int bls_set_entropy_source(const char* path);
 int bls_test_force_h2c_fallback(bls_ctx* ctx, const uint8_t* mask, size_t n);
 int bls_test_hash_to_g2_batch(bls_ctx* ctx, const uint8_t* msgs32, size_t n, uint8_t* out96);
 /* bls_test_miller_forms: the product of n pairings (48-B G1 / 96-B G2 encodings, no subgroup checks) through each
- * Miller-loop form of the batch path, final-exponentiated: out576 holds 7 x 576 bytes -- split lines +
+ * Miller-loop form of the batch path, final-exponentiated: out576 holds 8 x 576 bytes -- split lines +
  * accumulation (G = 2), fused (G = 2), fused (G = 1), split (G = 4), the wave-program kernel, split (G = 8),
- * split (G = 4, each step's lines multiplied together first).
+ * split (G = 4, each step's lines multiplied together first), split (G = 1 on eight lanes per f).
  * 1, or 0 on an invalid encoding. */
 int bls_test_miller_forms(bls_ctx* ctx, const uint8_t* g1s48, const uint8_t* g2s96, size_t n, uint8_t* out576);
 /* the same through the one-wave-per-message kernel of the per-call path */

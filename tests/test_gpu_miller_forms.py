@@ -1,6 +1,7 @@
 """GPU parity of the Miller-loop forms of the batch path (bls_test_miller_forms): the split kernels (the G2 lines of
 k_miller_lines2 + the f accumulation of k_miller_acc4q, two, four or eight pairs per f, and k_miller_acc4l: four
-pairs per f with each step's lines multiplied together before they meet f), the fused kernel
+pairs per f with each step's lines multiplied together before they meet f; k_miller_acc8: one pair per f on eight
+lanes), the fused kernel
 (k_miller_fused: lines formed in LDS by a line wave, one or two pairs per f) and the wave-program kernel of
 bls_multi_pairing -- the final exponentiation of each form's product must be the same GT element, and equal the
 oracle's pairing product (oracle/bls_oracle.py).  Pair counts are chosen off every multiple the kernels group by
@@ -14,7 +15,7 @@ from oracle import bls_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-FORMS = ("split G=2", "fused G=2", "fused G=1", "split G=4", "wave program", "split G=8", "split G=4 lines first")
+FORMS = ("split G=2", "fused G=2", "fused G=1", "split G=4", "wave program", "split G=8", "split G=4 lines first", "split G=1 eight lanes")
 
 
 def _gt_bytes(f):
