@@ -35,6 +35,7 @@ __global__ void __launch_bounds__(64) k_miller_lines2(const G2A* Q, size_t n, si
   const size_t step = (size_t)ML_WORDS * ld;
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
+    __asm__ volatile("" : "+v"(Li));  // no per-row induction pointers carried across the loop
     T.dbl(Li, ld);
     Li += step;
     if ((X_ABS >> b) & 1ull) {

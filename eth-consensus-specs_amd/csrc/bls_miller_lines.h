@@ -41,10 +41,11 @@ __device__ __forceinline__ Fq2B<V, D> bcp(const Fq2B<V, D>& a) {
 template <uint64_t V, uint64_t D>
 __device__ __forceinline__ void ml_store_q(uint32_t* L, size_t n, int w0, const Fq2B<V, D>& v) {
   const Fq2B<ML_LV, ML_LD> a = relax<ML_LV, ML_LD>(v);
+  uint32_t* const Lw = L + (size_t)w0 * n;  // a per-lane row base, so the row offsets are uniform
 #pragma unroll
   for (int j = 0; j < 14; ++j) {
-    L[(size_t)(w0 + j) * n] = a.c0.x.d[j];
-    L[(size_t)(w0 + 14 + j) * n] = a.c1.x.d[j];
+    Lw[(size_t)j * n] = a.c0.x.d[j];
+    Lw[(size_t)(14 + j) * n] = a.c1.x.d[j];
   }
 }
 

@@ -169,9 +169,9 @@ __device__ __forceinline__ LineIn ld_line(const uint32_t* Li, size_t n, bool h, 
     r.l0.c0.x.d[j] = Li[(size_t)j * n];
     r.l0.c1.x.d[j] = Li[(size_t)(14 + j) * n];
   }
-  const int w0 = (h ? 56 : 28) + (q ? 14 : 0);
+  const uint32_t* Lc = Li + (size_t)((h ? 56 : 28) + (q ? 14 : 0)) * n;  // per-lane row base: uniform row offsets
 #pragma unroll
-  for (int j = 0; j < 14; ++j) r.c.x.d[j] = Li[(size_t)(w0 + j) * n];
+  for (int j = 0; j < 14; ++j) r.c.x.d[j] = Lc[(size_t)j * n];
   return r;
 }
 
