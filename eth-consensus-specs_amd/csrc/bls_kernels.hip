@@ -93,6 +93,52 @@ __global__ void __launch_bounds__(NT) k_g1_sum_aff(const G1A* in, const int* ok,
   if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
 }
 
+// The sum of up to G1Q_SUM_MAX points in ONE workgroup (the per-call aggregate key, AggregatePKs, multi_exp
+// totals): each lane adds its points with the complete mixed additions of the registry gather in the redundant
+// digit form (bls_fq_g1.h g1q_add_aff), then a tree over the workgroup's lanes through LDS (g1q_add); the
+// projective (X : Y : Z) leaves as the Jacobian (X Z, Y Z^2, Z), packed.  One launch instead of two, and digit-form
+// products instead of packed ones (k_g1_sum_aff + k_jac_sum: 0.20-0.29 ms for 512 keys).
+constexpr int G1Q_SUM_NT = 256;
+constexpr size_t G1Q_SUM_MAX = 8 * G1Q_SUM_NT;
+__global__ void __launch_bounds__(G1Q_SUM_NT) k_g1_sum_q(const G1A* in, const int* ok, size_t n, G1J* out) {
+  __shared__ uint32_t sh[42][G1Q_SUM_NT];  // [word][lane]: a G1Q is 3 x 14 digits
+  const int t = (int)threadIdx.x;
+  const Fq zero = fq_zero();
+  G1Q acc{zero, fq_unpack(FP_ONE), zero};  // the identity (0 : 1 : 0)
+  for (size_t i = (size_t)t; i < n; i += G1Q_SUM_NT) {
+    if ((ok && !ok[i]) || in[i].inf) continue;
+    acc = g1q_add_aff(acc, fq_unpack(in[i].x), fq_unpack(in[i].y));
+  }
+  for (int s = G1Q_SUM_NT / 2; s > 0; s >>= 1) {
+    if (t >= s && t < 2 * s) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(&acc);
+#pragma unroll
+      for (int k = 0; k < 42; ++k) sh[k][t - s] = w[k];
+    }
+    __syncthreads();
+    if (t < s) {
+      G1Q o;
+      uint32_t* w = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int k = 0; k < 42; ++k) w[k] = sh[k][t];
+      acc = g1q_add(acc, o);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    G1J r;
+    const Fp z = fq_pack(acc.z);
+    if (fp_is_zero(z)) {
+      r = jac_identity<Fp>();
+    } else {
+      r.x = fq_pack(fq_mul(acc.x, acc.z));
+      r.y = fq_pack(fq_mul(fq_mul(acc.y, acc.z), acc.z));
+      r.z = z;
+    }
+    *out = r;
+  }
+}
+
 template <class F, int NT>
 __global__ void __launch_bounds__(NT) k_jac_sum(const Jac<F>* in, size_t n, Jac<F>* out) {
   __shared__ Jac<F> sh[NT];
@@ -480,6 +526,10 @@ hipError_t launch_key_validate(hipStream_t st, const uint8_t* pks, size_t n, G1A
 
 // Two-pass sums; tmp must hold >= 1 + nblk entries.
 hipError_t launch_g1_sum_aff(hipStream_t st, const G1A* in, const int* ok, size_t n, G1J* tmp, G1J* out) {
+  if (n <= G1Q_SUM_MAX) {
+    LAUNCH(k_g1_sum_q, 1, G1Q_SUM_NT, st, in, ok, n, out);
+    return hipSuccess;
+  }
   unsigned g = nblk(n, 64);
   if (g > 1024) g = 1024;
   if (g == 0) g = 1;
