@@ -15,7 +15,8 @@ from oracle import bls_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-FORMS = ("split G=2", "fused G=2", "fused G=1", "split G=4", "wave program", "split G=8", "split G=4 lines first", "split G=1 eight lanes")
+FORMS = ("split G=2", "fused G=2", "fused G=1", "split G=4", "wave program", "split G=8", "split G=4 lines first",
+         "split G=1 eight lanes")
 
 
 def _gt_bytes(f):
